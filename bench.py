@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Headline benchmark: forward+logdetJ samples/s of the fused MI355X FlowChain
+pass (BASELINE.json metric, configs[1]: d=5, 8 RealNVP layers, hidden 64,
+batch 2^20 fp32 per GPU).
+
+One "step" = one fused chain pass (df_chain_forward: x and ldj written) over
+the rank's batch, inputs already resident in HBM.  Multi-GPU (torchrun, one
+rank per GPU): every rank processes its own 2^20-sample shard (config 3:
+8·2^20 over 8 GPUs) with no data-path collective — weak scaling; timing is the
+max over ranks between barriers.  ``--mode nll`` benches the config-3 NLL step
+instead (fused inverse + logpdf + fp64 Σ, then an RCCL all-reduce of
+{Σ logpdf, count}).
+
+Rank 0 prints ONE JSON line (bench contract).  Extra objects:
+  roofline     — the fused kernel against the f32 MFMA peak (it is compute-
+                 bound: 3,212 FLOP/B algorithmic intensity); achieved = 2·ΣMAC
+                 per sample × samples per launch ÷ mean launch time from HIP
+                 events on the launch stream.
+  cpu_baseline — the oracle's Flux-like fp32 numpy restatement (BLAS sgemm,
+                 unfused op sequence) timed on the host cores on a bounded
+                 sample (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "forward+logdetJ Msamples/s, d=5 8-layer RealNVP, 1/2/4/8 MI355X"
+PEAK_F32_TFLOPS = 157.3   # MI355X f32 MFMA dense peak (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def build_chain(seed=2):
+    """Config 2: FlowChain(CouplingBlock, 4, 5; hidden_dim_s=64, hidden_dim_t=64).
+    Random init: Flux glorot_uniform weights; biases U(-0.1, 0.1); the final
+    Dense of each conditioner scaled by 0.1 so the 8-layer flow stays finite."""
+    import densityflows_amd as dfa
+
+    rng = np.random.default_rng(seed)
+    chain = dfa.FlowChain.repeat(dfa.CouplingBlock, 4, 5, hidden_dim_s=64, hidden_dim_t=64, rng=rng)
+    for blk in chain:
+        for layer in (blk.layer_1, blk.layer_2):
+            for net in (layer.s_net, layer.t_net):
+                for D in net:
+                    D.b = ((rng.random(D.out_dim) * 2 - 1) * 0.1).astype(np.float32)
+                net[-1].W = (net[-1].W * np.float32(0.1)).astype(np.float32)
+    return chain
+
+
+def cpu_baseline(chain, seconds=12.0, sample=65536):
+    """Oracle fp32 (Flux-like) forward+logdetJ on host cores, bounded sample."""
+    from oracle import flow_oracle as O
+
+    try:
+        from threadpoolctl import threadpool_info
+
+        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("internal_api") == "openblas"]
+                      or [1])
+    except Exception:  # pragma: no cover
+        threads = 1
+    spec = chain.to_spec()
+    rng = np.random.default_rng(0)
+    z = rng.standard_normal((5, sample)).astype(np.float32)
+    th = np.zeros((0, sample), np.float32)
+    O.forward(spec, z[:, :1024], th[:, :1024], np.float32)  # warm-up
+    done, t0 = 0, time.perf_counter()
+    while True:
+        O.forward(spec, z, th, np.float32)
+        done += sample
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": int(threads), "kind": "port",
+            "sample": f"{done} samples ({done // sample} passes of a {sample}-sample batch, config 2, "
+                      f"numpy fp32 oracle with OpenBLAS sgemm) in {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="samples per GPU")
+    ap.add_argument("--mode", choices=["forward", "nll"], default="forward")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    import densityflows_amd as dfa
+    from densityflows_amd.hip import HIPChain
+
+    chain = build_chain()
+    hc = chain.hip(device=local)
+    info = hc.info
+    B = args.batch
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    zbuf = torch.randn(B * 5, device=dev, generator=gen)      # Julia (5, B) column-major
+    xbuf = torch.empty_like(zbuf)
+    ldj = torch.empty(B, device=dev)
+    s64 = torch.zeros(2, dtype=torch.float64, device=dev)
+
+    if args.mode == "forward":
+        def step():
+            hc.run("forward", zbuf, None, xbuf, ldj, B)
+    else:
+        flow = dfa.Flow(chain, metadata=dfa.MetaData("", 5, 0, np.zeros(0, np.float32), np.zeros(0, np.float32)))
+        fh = flow.hip(device=local)
+        hc.run("forward", zbuf, None, xbuf, ldj, B)  # data points x = forward(z)
+
+        def step():
+            fh.run_logpdf_sum(xbuf, None, s64[:1], B)
+            s64[1] = float(B)
+            if dist is not None:
+                dist.all_reduce(s64)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)                 # HIP events on the launch stream
+    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    total = B * world * args.steps
+    value = total / elapsed / 1e6
+    kernel_s = gpu_ms / 1e3 / args.steps            # mean launch time (one launch per step)
+    flop = info.flops_per_sample * B
+    achieved_tflops = flop / kernel_s / 1e12
+    hbm_algo = 44.0 * B                              # read z (20 B) + write x (20 B) + ldj (4 B)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC if args.mode == "forward" else "NLL (inverse+logpdf+Σ, RCCL all-reduce) Msamples/s",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: z ~ N(0,1) generated on device; random-init weights (glorot, see bench.build_chain)",
+            "config": {"workload": "config2: d=5, n=0, FlowChain(CouplingBlock, 4, 5; hidden 64) = 8 RealNVP "
+                                   "layers, fp32" + ("" if world == 1 else f"; config3 sharding {world}x"),
+                       "per_gpu_batch": B, "global_batch": B * world,
+                       "parallelism": f"dp{world} (independent sample shards, no data-path collective)"
+                       if args.mode == "forward" else f"dp{world} + RCCL all-reduce of the NLL partial"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": PEAK_F32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_F32_TFLOPS, 4),
+                         "traffic": None,
+                         "kernel_ms": round(kernel_s * 1e3, 4),
+                         "algorithmic_flop_per_sample": info.flops_per_sample,
+                         "hbm_algorithmic_GBps": round(hbm_algo / kernel_s / 1e9, 2)},
+        }
+        if world == 1 and not args.no_cpu and args.mode == "forward":
+            out["cpu_baseline"] = cpu_baseline(chain, seconds=args.cpu_seconds)
+            out["vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

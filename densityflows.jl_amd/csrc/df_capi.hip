@@ -1,0 +1,348 @@
+// df_capi.hip — the C ABI declared in include/densityflows_hip.h.
+//
+// Host-side only: builds the packed plan (df_plan.cpp), owns the device copy
+// of it, and launches the fused kernels (df_kernels_ht*.hip).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "densityflows_hip.h"
+#include "df_kernels.h"
+#include "df_plan.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_err(hipError_t e, const char* where) {
+    return set_err(DF_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) == hipSuccess && (prev == dev || hipSetDevice(dev) == hipSuccess)) ok = true;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+template <typename T>
+int upload(const std::vector<T>& v, void** dst) {
+    size_t bytes = v.size() * sizeof(T);
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(dst, bytes);
+    if (e != hipSuccess) return set_err(DF_ERR_NOMEM, "hipMalloc failed for the chain plan");
+    if (!v.empty()) {
+        e = hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_err(e, "hipMemcpy(plan)");
+    }
+    return DF_OK;
+}
+
+constexpr double kLog2Pi = 1.8378770664093453;  // log(2π)
+
+}  // namespace
+
+struct df_chain {
+    df::Plan plan;
+    int device = 0;
+    void* d_layers = nullptr;
+    void* d_denses = nullptr;
+    void* d_chunks = nullptr;
+    void* d_stages = nullptr;
+    void* d_blob = nullptr;
+    void* d_tables = nullptr;
+    void* d_params = nullptr;
+    float* d_bounds = nullptr;  // [θmin (n) | θmax (n)]
+    bool has_bounds = false;
+    double* d_partial = nullptr;
+    int64_t partial_cap = 0;
+    int stage_bytes = 0;
+    int tab_bytes = 0;
+    size_t lds = 0;
+};
+
+extern "C" {
+
+int df_get_abi_version(void) { return DF_ABI_VERSION; }
+
+const char* df_last_error(void) { return g_err.c_str(); }
+
+int df_get_limits(df_limits* out) {
+    if (!out) return set_err(DF_ERR_INVALID, "null pointer");
+    out->max_state = df::kMaxState;
+    out->max_hidden = df::kMaxHidden;
+    out->max_af = df::kMaxAf;
+    out->max_layers = df::kMaxLayers;
+    return DF_OK;
+}
+
+int df_chain_destroy(df_chain* c) {
+    if (!c) return DF_OK;
+    DeviceGuard gd(c->device);
+    void* ptrs[] = {c->d_layers, c->d_denses, c->d_chunks, c->d_stages, c->d_blob,
+                    c->d_tables, c->d_params, c->d_bounds, c->d_partial};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    delete c;
+    return DF_OK;
+}
+
+int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
+    if (!out) return set_err(DF_ERR_INVALID, "null output handle");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return set_err(DF_ERR_HIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return set_err(DF_ERR_INVALID, "device ordinal out of range");
+    df_chain* c = new (std::nothrow) df_chain();
+    if (!c) return set_err(DF_ERR_NOMEM, "host allocation failed");
+    std::string err;
+    int rc = df::build_plan(desc, &c->plan, &err);
+    if (rc != DF_OK) {
+        delete c;
+        return set_err(rc, err);
+    }
+    c->device = device;
+    DeviceGuard gd(device);
+    if (!gd.ok) {
+        delete c;
+        return set_err(DF_ERR_HIP, "hipSetDevice failed");
+    }
+    const df::Plan& P = c->plan;
+    if ((rc = upload(P.layers, &c->d_layers)) != DF_OK || (rc = upload(P.denses, &c->d_denses)) != DF_OK ||
+        (rc = upload(P.chunks, &c->d_chunks)) != DF_OK || (rc = upload(P.stages, &c->d_stages)) != DF_OK ||
+        (rc = upload(P.blob, &c->d_blob)) != DF_OK || (rc = upload(P.tables, &c->d_tables)) != DF_OK ||
+        (rc = upload(P.params, &c->d_params)) != DF_OK) {
+        std::string m = g_err;
+        df_chain_destroy(c);
+        return set_err(rc, m);
+    }
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->d_bounds), sizeof(float) * (2 * P.n + 4));
+    if (e != hipSuccess) {
+        df_chain_destroy(c);
+        return set_err(DF_ERR_NOMEM, "hipMalloc failed (θ bounds)");
+    }
+    // LDS carve: [stage buffer | tables | state tile]; the stage area also hosts the
+    // fp64 workgroup reduction of the logpdf epilogue (>= 64 B).
+    c->stage_bytes = (P.stage_max + 15) / 16 * 16;
+    if (c->stage_bytes < 64) c->stage_bytes = 64;
+    c->tab_bytes = ((int)P.tables.size() * 4 + 15) / 16 * 16;
+    c->lds = (size_t)c->stage_bytes + c->tab_bytes + (size_t)P.samples_per_block * P.stride * 4;
+    if (c->lds > 160 * 1024) {
+        df_chain_destroy(c);
+        return set_err(DF_ERR_UNSUPPORTED, "chain needs more than 160 KiB of LDS per workgroup");
+    }
+    e = df::set_kernel_lds_limit(P.ht, c->lds);
+    if (e != hipSuccess) {
+        df_chain_destroy(c);
+        return hip_err(e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+    }
+    *out = c;
+    return DF_OK;
+}
+
+static void fill_info(const df::Plan& P, df_chain_info* out) {
+    out->d = P.d;
+    out->n = P.n;
+    out->n_layers = P.n_layers;
+    out->hidden_tiles = P.ht;
+    out->samples_per_block = P.samples_per_block;
+    out->n_stages = (int32_t)P.stages.size();
+    out->n_params = P.n_params;
+    out->flops_per_sample = P.flops_per_sample;
+    out->weight_bytes = (int64_t)P.blob.size();
+}
+
+int df_chain_get_info(const df_chain* c, df_chain_info* out) {
+    if (!c || !out) return set_err(DF_ERR_INVALID, "null pointer");
+    fill_info(c->plan, out);
+    return DF_OK;
+}
+
+int df_chain_validate(const df_chain_desc* desc, df_chain_info* info) {
+    df::Plan P;
+    std::string err;
+    int rc = df::build_plan(desc, &P, &err);
+    if (rc != DF_OK) return set_err(rc, err);
+    if (info) fill_info(P, info);
+    return DF_OK;
+}
+
+int df_chain_set_theta_bounds(df_chain* c, const float* tmin, const float* tmax) {
+    if (!c) return set_err(DF_ERR_INVALID, "null chain");
+    const int n = c->plan.n;
+    if (n == 0) {
+        c->has_bounds = false;
+        return DF_OK;
+    }
+    if (!tmin || !tmax) return set_err(DF_ERR_INVALID, "null θ bounds");
+    std::vector<float> b(2 * n);
+    std::memcpy(b.data(), tmin, sizeof(float) * n);
+    std::memcpy(b.data() + n, tmax, sizeof(float) * n);
+    DeviceGuard gd(c->device);
+    hipError_t e = hipMemcpy(c->d_bounds, b.data(), sizeof(float) * 2 * n, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_err(e, "hipMemcpy(θ bounds)");
+    c->has_bounds = true;
+    return DF_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, float* xout, float* ldj,
+        float* lp, double* sum_out, int64_t batch, void* stream) {
+    if (!c) return set_err(DF_ERR_INVALID, "null chain");
+    if (batch < 0) return set_err(DF_ERR_SHAPE, "negative batch size");
+    const df::Plan& P = c->plan;
+    if (batch == 0) {
+        if (sum_out) {
+            DeviceGuard gd(c->device);
+            hipError_t e = hipMemsetAsync(sum_out, 0, sizeof(double), (hipStream_t)stream);
+            if (e != hipSuccess) return hip_err(e, "hipMemsetAsync");
+        }
+        return DF_OK;
+    }
+    if (!zin) return set_err(DF_ERR_INVALID, "null input array");
+    if (P.n > 0 && !theta)
+        return set_err(DF_ERR_SHAPE, "dimensions θ must match (n, dims...) with n number of trained parameters");
+    if (mode != df::MODE_LOGPDF && !xout) return set_err(DF_ERR_INVALID, "null output array");
+    if (flow && P.n > 0 && !c->has_bounds) return set_err(DF_ERR_INVALID, "θ bounds not set (df_chain_set_theta_bounds)");
+
+    DeviceGuard gd(c->device);
+    if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
+    const int64_t S = P.samples_per_block;
+    const int64_t grid = (batch + S - 1) / S;
+    if (grid > 0x7fffffff) return set_err(DF_ERR_UNSUPPORTED, "batch too large for one launch");
+    if (sum_out && grid > c->partial_cap) {
+        if (c->d_partial) (void)hipFree(c->d_partial);
+        c->d_partial = nullptr;
+        c->partial_cap = 0;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->d_partial), sizeof(double) * grid);
+        if (e != hipSuccess) return set_err(DF_ERR_NOMEM, "hipMalloc failed (NLL partials)");
+        c->partial_cap = grid;
+    }
+
+    df::ChainArgs a{};
+    a.zin = zin;
+    a.theta = theta;
+    a.xout = xout;
+    a.ldj_out = ldj;
+    a.lp_out = lp;
+    a.partial = sum_out ? c->d_partial : nullptr;
+    a.batch = batch;
+    a.layers = static_cast<const df::DevLayer*>(c->d_layers);
+    a.denses = static_cast<const df::DevDense*>(c->d_denses);
+    a.chunks = static_cast<const df::DevChunk*>(c->d_chunks);
+    a.stages = static_cast<const df::DevStage*>(c->d_stages);
+    a.blob = static_cast<const uint8_t*>(c->d_blob);
+    a.tables = static_cast<const int32_t*>(c->d_tables);
+    a.params = static_cast<const float*>(c->d_params);
+    a.tmin = (flow && P.n > 0) ? c->d_bounds : nullptr;
+    a.tmax = (flow && P.n > 0) ? c->d_bounds + P.n : nullptr;
+    a.d = P.d;
+    a.n = P.n;
+    a.stride = P.stride;
+    a.n_layers = P.n_layers;
+    a.tab_ints = (int)P.tables.size();
+    a.tab_bytes = c->tab_bytes;
+    a.stage_bytes = c->stage_bytes;
+    // Distributions.mvnormal_c0: -(d * log2π + logdetcov)/2 in Float32, logdet(I) = 0
+    a.c0 = -((float)P.d * (float)kLog2Pi + 0.f) / 2.f;
+
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipError_t e = df::launch_chain(P.ht, mode, P.outv != 0, a, (unsigned)grid, c->lds, st);
+    if (e != hipSuccess) return hip_err(e, "chain kernel launch");
+    if (sum_out) {
+        e = df::launch_reduce_partials(c->d_partial, grid, sum_out, st);
+        if (e != hipSuccess) return hip_err(e, "reduce kernel launch");
+    }
+    return DF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int df_chain_forward(df_chain* c, const float* z, const float* theta, float* x_out, float* ldj_out, int64_t batch,
+                     void* stream) {
+    return run(c, df::MODE_FWD, false, z, theta, x_out, ldj_out, nullptr, nullptr, batch, stream);
+}
+
+int df_chain_backward(df_chain* c, const float* x, const float* theta, float* z_out, float* ldj_out, int64_t batch,
+                      void* stream) {
+    return run(c, df::MODE_BWD, false, x, theta, z_out, ldj_out, nullptr, nullptr, batch, stream);
+}
+
+int df_chain_forward_inplace(df_chain* c, float* z, const float* theta, int64_t batch, void* stream) {
+    return run(c, df::MODE_FWD_INPLACE, false, z, theta, z, nullptr, nullptr, nullptr, batch, stream);
+}
+
+int df_flow_forward(df_chain* c, const float* z, const float* theta_raw, float* x_out, float* ldj_out,
+                    int64_t batch, void* stream) {
+    return run(c, df::MODE_FWD, true, z, theta_raw, x_out, ldj_out, nullptr, nullptr, batch, stream);
+}
+
+int df_flow_backward(df_chain* c, const float* x, const float* theta_raw, float* z_out, float* ldj_out,
+                     int64_t batch, void* stream) {
+    return run(c, df::MODE_BWD, true, x, theta_raw, z_out, ldj_out, nullptr, nullptr, batch, stream);
+}
+
+int df_flow_forward_inplace(df_chain* c, float* z, const float* theta_raw, int64_t batch, void* stream) {
+    return run(c, df::MODE_FWD_INPLACE, true, z, theta_raw, z, nullptr, nullptr, nullptr, batch, stream);
+}
+
+int df_flow_logpdf(df_chain* c, const float* x, const float* theta_raw, float* logpdf_out, int64_t batch,
+                   void* stream) {
+    if (batch > 0 && !logpdf_out) return set_err(DF_ERR_INVALID, "null logpdf output");
+    return run(c, df::MODE_LOGPDF, true, x, theta_raw, nullptr, nullptr, logpdf_out, nullptr, batch, stream);
+}
+
+int df_flow_logpdf_sum(df_chain* c, const float* x, const float* theta_raw, double* sum_out, int64_t batch,
+                       void* stream) {
+    if (!sum_out) return set_err(DF_ERR_INVALID, "null sum output");
+    return run(c, df::MODE_LOGPDF, true, x, theta_raw, nullptr, nullptr, nullptr, sum_out, batch, stream);
+}
+
+int df_device_alloc(void** ptr, size_t bytes) {
+    if (!ptr) return set_err(DF_ERR_INVALID, "null pointer");
+    hipError_t e = hipMalloc(ptr, bytes ? bytes : 1);
+    return e == hipSuccess ? DF_OK : set_err(DF_ERR_NOMEM, "hipMalloc failed");
+}
+
+int df_device_free(void* ptr) {
+    hipError_t e = hipFree(ptr);
+    return e == hipSuccess ? DF_OK : hip_err(e, "hipFree");
+}
+
+int df_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+    return e == hipSuccess ? DF_OK : hip_err(e, "hipMemcpyAsync(H2D)");
+}
+
+int df_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+    return e == hipSuccess ? DF_OK : hip_err(e, "hipMemcpyAsync(D2H)");
+}
+
+int df_stream_synchronize(void* stream) {
+    hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    return e == hipSuccess ? DF_OK : hip_err(e, "hipStreamSynchronize");
+}
+
+}  // extern "C"

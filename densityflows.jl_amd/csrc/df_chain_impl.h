@@ -1,0 +1,581 @@
+// df_chain_impl.h — fused CDNA4 (gfx950) kernel for the DensityFlows.jl
+// FlowChain hot path: forward / backward (inverse) / forward! / logpdf.
+// Included once per kernel variant (DF_HT) by df_kernels_ht*.hip.
+//
+// One workgroup (8 waves) owns S = 8·16·T consecutive samples.  Their state
+// rows [θ | z | 0] live in LDS for the whole chain; each wave owns 16·T rows.
+// Per coupling layer (src/affine/RNVP.jl:168-205, NICE.jl:118-170):
+//   * the conditioner input vcat(θ,z)[axis_nn] is gathered from LDS through a
+//     per-layer slot table (bit-exact index selection);
+//   * every Dense of the s and t nets runs on v_mfma_f32_16x16x4_f32 with the
+//     samples as the MFMA column dimension: A = weight fragments read from the
+//     LDS stage buffer (packed by df_plan.cpp), B = activations held in
+//     registers.  An accumulator tile is directly the B operand of the next
+//     Dense (k = 16·tile + 4·lane_group + reg), so activations never leave
+//     registers;
+//   * bias (W*x .+ b, added after the product as Flux does) and σ are applied
+//     to the accumulators; a final Dense with <= 4 outputs is a VALU GEMV;
+//   * the coupling x_af = z_af·exp(s) + t is applied in two in-place phases,
+//     one right after each net: forward  z·exp(s) (s-net) then + t (t-net);
+//     inverse (x - t) (t-net) then ·exp(-s) (s-net).  Julia rounds the
+//     product and the sum separately, so the phases are bit-identical to the
+//     fused expression, and the conditioner input never contains transformed
+//     dims (planner check), so the second net sees the same input;
+//   * ldj = ±Σ s is accumulated per FlowElement and chain exactly as the
+//     reference groups it (Blocks.jl:136,149, Chains.jl:160,179).
+// Weights are staged global→LDS in stages (several layers per stage when they
+// fit); the stage cache is uniform across the workgroup.
+//
+// Compiled with -ffp-contract=off: element-wise arithmetic is rounded op by
+// op as Julia does (no implicit FMA); the MFMA products are exact f32 FMA
+// chains.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "df_kernels.h"
+
+namespace df {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef DF_WAVES_PER_EU
+#define DF_WAVES_PER_EU(HT) ((HT) <= 4 ? 4 : 2)
+#endif
+
+namespace impl {
+
+__device__ __forceinline__ float relu(float x) { return (x > 0.f) ? x : ((x == x) ? 0.f : x); }
+
+__device__ __noinline__ float act_fn(int act, float x) {
+    switch (act) {
+        case DF_ACT_IDENTITY: return x;
+        case DF_ACT_RELU: return relu(x);  // max(0, x), NaN-propagating
+        case DF_ACT_TANH: return tanhf(x);
+        case DF_ACT_SIGMOID: {  // NNlib.sigmoid
+            float t = expf(-fabsf(x));
+            return (x >= 0.f) ? 1.f / (1.f + t) : t / (1.f + t);
+        }
+        case DF_ACT_SOFTPLUS: return log1pf(expf(-fabsf(x))) + ((x > 0.f) ? x : 0.f);
+        case DF_ACT_LOGCOSH: {  // x + softplus(-2x) - log(2)
+            float y = -2.f * x;
+            float sp = log1pf(expf(-fabsf(y))) + ((y > 0.f) ? y : 0.f);
+            return (x + sp) - 0.6931471805599453f;
+        }
+        case DF_ACT_LEAKYRELU: return (x > 0.f) ? x : 0.01f * x;
+        case DF_ACT_ELU: return (x > 0.f) ? x : expm1f(x);
+        case DF_ACT_SWISH: {
+            float t = expf(-fabsf(x));
+            float sg = (x >= 0.f) ? 1.f / (1.f + t) : t / (1.f + t);
+            return x * sg;
+        }
+        default: return x;
+    }
+}
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 lds4(const uint8_t* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+struct Smem {
+    uint8_t* stage;
+    const int32_t* tab;
+    float* state;
+};
+
+// Copy stage `s` of the weight blob into the LDS stage buffer (uniform).
+__device__ __forceinline__ void ensure_stage(int s, int& cur, const ChainArgs& a, uint8_t* buf) {
+    if (s == cur) return;
+    __syncthreads();  // every wave is done with the previous stage
+    const DevStage st = a.stages[s];
+    const f32x4* src = reinterpret_cast<const f32x4*>(a.blob + st.src_off);
+    f32x4* dst = reinterpret_cast<f32x4*>(buf);
+    const int n16 = st.bytes >> 4;
+    for (int i = threadIdx.x; i < n16; i += kBlockThreads) dst[i] = src[i];
+    __syncthreads();
+    cur = s;
+}
+
+constexpr int out_tiles(int HT) { return HT < 2 ? HT : 2; }
+
+template <int HT, int T, bool OUTV>
+struct NetRegs {
+    f32x4 h[T][HT];    // activations of the previous Dense (B operands)
+    f32x4 acc[T][HT];  // accumulators of the current Dense
+    // net output: OUTV: out[tt][0] = (o0..o3) in every lane group;
+    // MFMA path: out[tt][m] = rows 16m + 4g + r
+    f32x4 out[T][OUTV ? 1 : out_tiles(HT)];
+};
+
+// One MFMA Dense: acc = W · input (+ b, σ).  IN_STATE gathers the input
+// features of vcat(θ,z)[axis_nn] from the LDS state rows.
+template <int HT, int T>
+__device__ __forceinline__ void dense_mfma(const ChainArgs& a, const DevDense& D, const int32_t* feat,
+                                           int& cur_stage, const Smem& sm, const int (&rowoff)[T],
+                                           f32x4 (&h)[T][HT], f32x4 (&acc)[T][HT]) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4;
+    constexpr int MG = (T == 1) ? 2 : 1;  // m-tiles per A-fragment group (independent MFMA chains)
+#pragma unroll
+    for (int tt = 0; tt < T; ++tt)
+#pragma unroll
+        for (int m = 0; m < HT; ++m) acc[tt][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int c = 0; c < D.n_chunks; ++c) {
+        const DevChunk C = a.chunks[D.chunk0 + c];
+        ensure_stage(C.stage, cur_stage, a, sm.stage);
+        const uint8_t* base = sm.stage + C.lds_off + lane * 16;
+        if (D.in_kind == IN_STATE) {
+#pragma unroll
+            for (int kq = 0; kq < kMaxState / 16; ++kq) {
+                if (kq >= C.kq_begin && kq < C.kq_end) {
+                    float xin[T][4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int s = 4 * kq + r;
+                        if (s < D.ks) {
+                            const int slot = feat[4 * s + g];
+#pragma unroll
+                            for (int tt = 0; tt < T; ++tt) xin[tt][r] = sm.state[rowoff[tt] + slot];
+                        } else {
+#pragma unroll
+                            for (int tt = 0; tt < T; ++tt) xin[tt][r] = 0.f;
+                        }
+                    }
+                    const uint8_t* bq = base + (kq - C.kq_begin) * D.mt * 1024;
+#pragma unroll
+                    for (int m0 = 0; m0 < HT; m0 += MG) {
+                        if (m0 < D.mt) {
+                            f32x4 w[MG];
+#pragma unroll
+                            for (int mm = 0; mm < MG; ++mm)
+                                w[mm] = (m0 + mm < D.mt) ? lds4(bq + (m0 + mm) * 1024) : f32x4{0, 0, 0, 0};
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                if (4 * kq + r < D.ks) {
+#pragma unroll
+                                    for (int mm = 0; mm < MG; ++mm)
+                                        if (m0 + mm < HT && m0 + mm < D.mt)
+#pragma unroll
+                                            for (int tt = 0; tt < T; ++tt)
+                                                acc[tt][m0 + mm] = mfma4(w[mm][r], xin[tt][r], acc[tt][m0 + mm]);
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        } else if (D.mt == HT && C.kq_begin == 0 && C.kq_end == HT) {
+            // full-width hidden Dense in one stage: guard-free, fully unrolled
+#pragma unroll
+            for (int kq = 0; kq < HT; ++kq) {
+#pragma unroll
+                for (int m = 0; m < HT; ++m) {
+                    const f32x4 w = lds4(base + (kq * HT + m) * 1024);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int tt = 0; tt < T; ++tt) acc[tt][m] = mfma4(w[r], h[tt][kq][r], acc[tt][m]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int kq = 0; kq < HT; ++kq) {
+                if (kq >= C.kq_begin && kq < C.kq_end) {
+                    const uint8_t* bq = base + (kq - C.kq_begin) * D.mt * 1024;
+#pragma unroll
+                    for (int m0 = 0; m0 < HT; m0 += MG) {
+                        if (m0 < D.mt) {
+                            f32x4 w[MG];
+#pragma unroll
+                            for (int mm = 0; mm < MG; ++mm)
+                                w[mm] = (m0 + mm < D.mt) ? lds4(bq + (m0 + mm) * 1024) : f32x4{0, 0, 0, 0};
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                                for (int mm = 0; mm < MG; ++mm)
+                                    if (m0 + mm < HT && m0 + mm < D.mt)
+#pragma unroll
+                                        for (int tt = 0; tt < T; ++tt)
+                                            acc[tt][m0 + mm] = mfma4(w[mm][r], h[tt][kq][r], acc[tt][m0 + mm]);
+                        }
+                    }
+                }
+            }
+        }
+    }
+
+    // bias (after the product, as W*x .+ b) and activation
+    ensure_stage(D.bias_stage, cur_stage, a, sm.stage);
+    if (D.has_bias) {
+#pragma unroll
+        for (int m = 0; m < HT; ++m) {
+            if (m < D.mt) {
+                const f32x4 b = lds4(sm.stage + D.bias_lds + ((16 * m + 4 * g) << 2));
+#pragma unroll
+                for (int tt = 0; tt < T; ++tt) acc[tt][m] = acc[tt][m] + b;
+            }
+        }
+    }
+    if (D.act == DF_ACT_RELU) {
+#pragma unroll
+        for (int m = 0; m < HT; ++m)
+#pragma unroll
+            for (int tt = 0; tt < T; ++tt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[tt][m][r] = relu(acc[tt][m][r]);
+    } else if (D.act != DF_ACT_IDENTITY) {
+#ifndef DF_NO_GENERIC_ACT
+#pragma unroll
+        for (int m = 0; m < HT; ++m) {
+            if (m < D.mt) {
+#pragma unroll
+                for (int tt = 0; tt < T; ++tt)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[tt][m][r] = act_fn(D.act, acc[tt][m][r]);
+            }
+        }
+#endif
+    }
+}
+
+// Evaluate one conditioner net (s or t) for this wave's T sample tiles into R.out.
+template <int HT, int T, bool OUTV>
+__device__ __forceinline__ void eval_net(const ChainArgs& a, const DevLayer& L, int dense0, int ndense,
+                                         int& cur_stage, const Smem& sm, const int (&rowoff)[T],
+                                         NetRegs<HT, T, OUTV>& R) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4;
+    const int32_t* feat = sm.tab + L.feat_tab;
+    for (int k = 0; k < ndense; ++k) {
+        const DevDense D = a.denses[dense0 + k];
+        if (OUTV && k + 1 == ndense) {
+            // ---- final Dense as a VALU GEMV: out[o] = Σ_k W[o][k] h[k] + b[o] ----
+            ensure_stage(D.w3_stage, cur_stage, a, sm.stage);
+            const uint8_t* w3 = sm.stage + D.w3_lds;
+            const int inp = 16 * D.kt_in;
+            const float* b3 = reinterpret_cast<const float*>(w3) + D.n_out * inp;
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                if (o < D.n_out) {
+                    float p[T];
+#pragma unroll
+                    for (int tt = 0; tt < T; ++tt) p[tt] = 0.f;
+#pragma unroll
+                    for (int kq = 0; kq < HT; ++kq) {
+                        if (kq < D.kt_in) {
+                            f32x4 w = lds4(w3 + ((o * inp + 16 * kq + 4 * g) << 2));
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                                for (int tt = 0; tt < T; ++tt) p[tt] = __builtin_fmaf(w[r], R.h[tt][kq][r], p[tt]);
+                        }
+                    }
+#pragma unroll
+                    for (int tt = 0; tt < T; ++tt) {
+                        p[tt] += __shfl_xor(p[tt], 16);
+                        p[tt] += __shfl_xor(p[tt], 32);
+                        float v = p[tt];
+                        if (D.has_bias) v = v + b3[o];
+                        R.out[tt][0][o] = act_fn(D.act, v);
+                    }
+                } else {
+#pragma unroll
+                    for (int tt = 0; tt < T; ++tt) R.out[tt][0][o] = 0.f;
+                }
+            }
+            return;
+        }
+        dense_mfma<HT, T>(a, D, feat, cur_stage, sm, rowoff, R.h, R.acc);
+        if (k + 1 == ndense) {
+            if constexpr (!OUTV) {
+#pragma unroll
+                for (int tt = 0; tt < T; ++tt)
+#pragma unroll
+                    for (int m = 0; m < out_tiles(HT); ++m) R.out[tt][m] = R.acc[tt][m];
+            }
+        } else {
+#pragma unroll
+            for (int tt = 0; tt < T; ++tt)
+#pragma unroll
+                for (int m = 0; m < HT; ++m) R.h[tt][m] = R.acc[tt][m];
+        }
+    }
+}
+
+__device__ __forceinline__ float sel4(const f32x4 v, int i) {
+    float r = v[0];
+    r = (i == 1) ? v[1] : r;
+    r = (i == 2) ? v[2] : r;
+    r = (i == 3) ? v[3] : r;
+    return r;
+}
+
+enum Phase { PH_S_FWD, PH_T_FWD, PH_T_BWD, PH_S_BWD };
+
+// Apply one coupling phase to the transformed dims of this wave's rows.
+// Returns Σ_k s[k] for the s phases (0 otherwise).
+template <int HT, int T, bool OUTV, int PH>
+__device__ __forceinline__ void couple_phase(const NetRegs<HT, T, OUTV>& R, const DevLayer& L, const Smem& sm,
+                                             const int (&rowoff)[T], float (&ssum)[T]) {
+    const int g = (threadIdx.x & 63) >> 4;
+    const int32_t* af = sm.tab + L.af_tab;
+    constexpr bool SPH = (PH == PH_S_FWD || PH == PH_S_BWD);
+    if constexpr (OUTV) {
+        // every lane holds out[0..3]; lane group g transforms dim axis_af[g]
+#pragma unroll
+        for (int tt = 0; tt < T; ++tt) {
+            const float y = sel4(R.out[tt][0], g);
+            if (g < L.n_af) {
+                const int slot = af[g];
+                float v = sm.state[rowoff[tt] + slot];
+                if (PH == PH_S_FWD) v = v * expf(y);
+                if (PH == PH_T_FWD) v = v + y;
+                if (PH == PH_T_BWD) v = v - y;
+                if (PH == PH_S_BWD) v = v * expf(-y);
+                sm.state[rowoff[tt] + slot] = v;
+            }
+            if (SPH) {
+                // ldj = Σ_k s[k] in row order (RNVP.jl:180 / :86)
+                float l = R.out[tt][0][0];
+#pragma unroll
+                for (int o = 1; o < 4; ++o)
+                    if (o < L.n_af) l = l + R.out[tt][0][o];
+                ssum[tt] = l;
+            }
+        }
+    } else {
+        constexpr int OT = out_tiles(HT);
+#pragma unroll
+        for (int tt = 0; tt < T; ++tt) {
+            float p = 0.f;
+#pragma unroll
+            for (int m = 0; m < OT; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int o = 16 * m + 4 * g + r;
+                    if (o < L.n_af) {
+                        const int slot = af[o];
+                        const float y = R.out[tt][m][r];
+                        float v = sm.state[rowoff[tt] + slot];
+                        if (PH == PH_S_FWD) v = v * expf(y);
+                        if (PH == PH_T_FWD) v = v + y;
+                        if (PH == PH_T_BWD) v = v - y;
+                        if (PH == PH_S_BWD) v = v * expf(-y);
+                        sm.state[rowoff[tt] + slot] = v;
+                        if (SPH) p = p + y;
+                    }
+                }
+            if (SPH) {
+                p += __shfl_xor(p, 16);
+                p += __shfl_xor(p, 32);
+                ssum[tt] = p;
+            }
+        }
+    }
+}
+
+}  // namespace impl
+
+template <int HT, int MODE, bool OUTV>
+__global__ void __launch_bounds__(kBlockThreads, DF_WAVES_PER_EU(HT))
+chain_kernel(ChainArgs a) {
+    using namespace impl;
+    constexpr int T = tiles_per_wave(HT);
+    constexpr bool FWD = (MODE == MODE_FWD || MODE == MODE_FWD_INPLACE);
+    constexpr bool WANT_LDJ = (MODE != MODE_FWD_INPLACE);
+    constexpr int S = kWavesPerBlock * 16 * T;
+
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    Smem sm;
+    sm.stage = smem;
+    int32_t* tab = reinterpret_cast<int32_t*>(smem + a.stage_bytes);
+    sm.tab = tab;
+    sm.state = reinterpret_cast<float*>(smem + a.stage_bytes + a.tab_bytes);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, j = lane & 15;
+    const int d = a.d, n = a.n, stride = a.stride, nd = n + d;
+    const int64_t s0 = (int64_t)blockIdx.x * S;
+    const int nvalid = (int)((a.batch - s0) < S ? (a.batch - s0) : S);
+
+    // ---- tables, state tile [θ | z | 0] ----
+    for (int i = tid; i < a.tab_ints; i += kBlockThreads) tab[i] = a.tables[i];
+    for (int i = tid; i < S * d; i += kBlockThreads) {
+        const int smp = i / d, c = i - smp * d;
+        float v = 0.f;
+        if (smp < nvalid) v = a.zin[(s0 + smp) * d + c];
+        sm.state[smp * stride + n + c] = v;
+    }
+    for (int i = tid; i < S * n; i += kBlockThreads) {
+        const int smp = i / n, c = i - smp * n;
+        float v = 0.f;
+        if (smp < nvalid) {
+            v = a.theta[(s0 + smp) * n + c];
+            if (a.tmin) {  // normalize_input: (θ - θmin) ./ (θmax - θmin), 0 where max == min (Data.jl:213-218)
+                const float lo = a.tmin[c], diff = a.tmax[c] - lo;
+                v = (diff == 0.f) ? 0.f : (v - lo) / diff;
+            }
+        }
+        sm.state[smp * stride + c] = v;
+    }
+    for (int i = tid; i < S; i += kBlockThreads)
+        for (int c = nd; c < stride; ++c) sm.state[i * stride + c] = 0.f;
+    __syncthreads();
+
+    int rowoff[T];
+#pragma unroll
+    for (int tt = 0; tt < T; ++tt) rowoff[tt] = ((wave * T + tt) * 16 + j) * stride;
+
+    float ldj_acc[T], ldj_e[T];
+#pragma unroll
+    for (int tt = 0; tt < T; ++tt) { ldj_acc[tt] = 0.f; ldj_e[tt] = 0.f; }
+    bool have_acc = false;
+    int cur_stage = -1;
+
+    NetRegs<HT, T, OUTV> R;
+    for (int it = 0; it < a.n_layers; ++it) {
+        const int li = FWD ? it : a.n_layers - 1 - it;
+        const DevLayer L = a.layers[li];
+        float lval[T];
+#pragma unroll
+        for (int tt = 0; tt < T; ++tt) lval[tt] = 0.f;
+        if (L.kind == DF_LAYER_NORM) {
+            // NormalizationLayer, src/norm/Normalization.jl:64-103
+            const float al = L.alpha, be = L.beta, delta = be - al;
+            const float* xmn = a.params + L.norm_off;
+            const float* xmx = xmn + d;
+#pragma unroll
+            for (int tt = 0; tt < T; ++tt) {
+                for (int i = g; i < d; i += 4) {
+                    const float lo = xmn[i], hi = xmx[i], xd = hi - lo;
+                    float v = sm.state[rowoff[tt] + n + i];
+                    if (FWD) v = ((xd * v - al * hi) + be * lo) / delta;
+                    else v = (be * (v - lo) + al * (hi - v)) / xd;
+                    sm.state[rowoff[tt] + n + i] = v;
+                }
+                lval[tt] = FWD ? L.ldj_const : -L.ldj_const;
+            }
+        } else {
+            const bool rnvp = (L.kind == DF_LAYER_RNVP);
+            float ssum[T];
+            if (FWD) {
+                if (rnvp) {
+                    eval_net<HT, T, OUTV>(a, L, L.s_dense0, L.s_ndense, cur_stage, sm, rowoff, R);
+                    couple_phase<HT, T, OUTV, PH_S_FWD>(R, L, sm, rowoff, ssum);
+#pragma unroll
+                    for (int tt = 0; tt < T; ++tt) lval[tt] = ssum[tt];
+                }
+                eval_net<HT, T, OUTV>(a, L, L.t_dense0, L.t_ndense, cur_stage, sm, rowoff, R);
+                couple_phase<HT, T, OUTV, PH_T_FWD>(R, L, sm, rowoff, ssum);
+            } else {
+                eval_net<HT, T, OUTV>(a, L, L.t_dense0, L.t_ndense, cur_stage, sm, rowoff, R);
+                couple_phase<HT, T, OUTV, PH_T_BWD>(R, L, sm, rowoff, ssum);
+                if (rnvp) {
+                    eval_net<HT, T, OUTV>(a, L, L.s_dense0, L.s_ndense, cur_stage, sm, rowoff, R);
+                    couple_phase<HT, T, OUTV, PH_S_BWD>(R, L, sm, rowoff, ssum);
+#pragma unroll
+                    for (int tt = 0; tt < T; ++tt) lval[tt] = -ssum[tt];  // ln_det_jac = -Σ s
+                }
+            }
+        }
+        if (WANT_LDJ) {
+            // FlowElement grouping: CouplingBlock ldj_1 .+ ldj_2, chain left fold
+            const bool first_in_elem = FWD ? L.elem_start : L.elem_end;
+            const bool last_in_elem = FWD ? L.elem_end : L.elem_start;
+#pragma unroll
+            for (int tt = 0; tt < T; ++tt) ldj_e[tt] = first_in_elem ? lval[tt] : ldj_e[tt] + lval[tt];
+            if (last_in_elem) {
+#pragma unroll
+                for (int tt = 0; tt < T; ++tt) ldj_acc[tt] = have_acc ? ldj_acc[tt] + ldj_e[tt] : ldj_e[tt];
+                have_acc = true;
+            }
+        }
+    }
+
+    // ---- epilogue ----
+    if (MODE == MODE_LOGPDF) {
+        // logpdf(MvNormal(0, I), z) .+ ldj = (c0 - Σ z²/2) + ldj   (Flows.jl:279)
+        double part = 0.0;
+#pragma unroll
+        for (int tt = 0; tt < T; ++tt) {
+            const int smp = (wave * T + tt) * 16 + j;
+            float q = 0.f;
+            for (int i = 0; i < d; ++i) {
+                const float zz = sm.state[rowoff[tt] + n + i];
+                q = q + zz * zz;
+            }
+            const float lp = (a.c0 - q / 2.f) + ldj_acc[tt];
+            if (g == 0 && smp < nvalid) {
+                if (a.lp_out) a.lp_out[s0 + smp] = lp;
+                part += (double)lp;
+            }
+        }
+        if (a.partial) {
+            // deterministic workgroup reduction in fp64
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off);
+            __syncthreads();
+            double* red = reinterpret_cast<double*>(smem);
+            if (lane == 0) red[wave] = part;
+            __syncthreads();
+            if (tid == 0) {
+                double s = 0.0;
+                for (int w = 0; w < kWavesPerBlock; ++w) s += red[w];
+                a.partial[blockIdx.x] = s;
+            }
+        }
+        if (!a.xout) return;
+    }
+    __syncthreads();
+    for (int i = tid; i < S * d; i += kBlockThreads) {
+        const int smp = i / d, c = i - smp * d;
+        if (smp < nvalid) a.xout[(s0 + smp) * d + c] = sm.state[smp * stride + n + c];
+    }
+    if (WANT_LDJ && MODE != MODE_LOGPDF && a.ldj_out && g == 0) {
+#pragma unroll
+        for (int tt = 0; tt < T; ++tt) {
+            const int smp = (wave * T + tt) * 16 + j;
+            if (smp < nvalid) a.ldj_out[s0 + smp] = ldj_acc[tt];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// per-variant host launchers
+// ---------------------------------------------------------------------------
+template <int HT>
+void* chain_kernel_ptr(int mode, bool outv) {
+#define DF_K(M) (outv ? reinterpret_cast<void*>(&chain_kernel<HT, M, true>) \
+                      : reinterpret_cast<void*>(&chain_kernel<HT, M, false>))
+    switch (mode) {
+        case MODE_FWD: return DF_K(MODE_FWD);
+        case MODE_FWD_INPLACE: return DF_K(MODE_FWD_INPLACE);
+        case MODE_BWD: return DF_K(MODE_BWD);
+        default: return DF_K(MODE_LOGPDF);
+    }
+#undef DF_K
+}
+
+template <int HT>
+hipError_t launch_chain_ht(int mode, bool outv, const ChainArgs& a, unsigned grid, size_t lds, hipStream_t st) {
+    void* f = chain_kernel_ptr<HT>(mode, outv);
+    void* args[] = {const_cast<ChainArgs*>(&a)};
+    return hipLaunchKernel(f, dim3(grid), dim3(kBlockThreads), args, lds, st);
+}
+
+template <int HT>
+hipError_t set_lds_limit_ht(size_t lds) {
+    for (int mode = 0; mode < 4; ++mode)
+        for (int ov = 0; ov < 2; ++ov) {
+            hipError_t e = hipFuncSetAttribute(chain_kernel_ptr<HT>(mode, ov != 0),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
+
+}  // namespace df

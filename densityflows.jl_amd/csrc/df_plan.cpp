@@ -1,0 +1,372 @@
+// df_plan.cpp — validate a df_chain_desc and pack it for the fused kernels.
+//
+// Reference semantics restated here (DensityFlows.jl v1.0.0):
+//   * conditioner input = vcat(θ, z)[axis_nn]        src/affine/RNVP.jl:157,174,196
+//     → the kernel keeps each sample's state row as [θ (n) | z (d) | 0] in LDS,
+//       so a 1-based axis_nn entry k is the state slot k-1; padding slot n+d is 0.
+//   * x_af = z_af .* exp.(s) .+ t, row k of s/t ↔ dim axis_af[k]   RNVP.jl:182-184
+//     → af table: slot n + axis_af[k] - 1.
+//   * s/t nets: Chain(Dense(in,h,σ), (n-1)×Dense(h,h,σ), Dense(h,out))  Layers.jl:33-50
+//   * Flux.Dense weight is (out, in) column-major: W[i + out*k].
+#include "df_plan.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <set>
+#include <sstream>
+
+namespace df {
+namespace {
+
+struct Fail {
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] void fail(int code, const std::string& m) { throw Fail{code, m}; }
+
+int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+int pow2_tiles(int t) {
+    int p = 1;
+    while (p < t) p *= 2;
+    return p;
+}
+
+// One packable item of a coupling layer, in kernel consumption order.
+struct Item {
+    enum Kind { CHUNK_KQ, BIAS, W3 } kind;
+    int dense;   // index into plan.denses
+    int kq;      // CHUNK_KQ: k-quad index
+    int bytes;
+};
+
+class Packer {
+public:
+    explicit Packer(Plan& p) : P(p) {}
+
+    int remaining() const { return cur_ < 0 ? 0 : kStageCap - used_; }
+
+    void begin_stage() {
+        close();
+        cur_ = (int)P.stages.size();
+        DevStage s{};
+        s.src_off = (int64_t)P.blob.size();
+        P.stages.push_back(s);
+        used_ = 0;
+    }
+
+    // Reserve `bytes` (multiple of 16) in the current stage (opening one if
+    // needed).  Returns {stage, byte offset in stage}.
+    std::pair<int, int> alloc(int bytes) {
+        if (bytes > kStageCap) fail(DF_ERR_UNSUPPORTED, "packed item exceeds the LDS stage buffer");
+        if (cur_ < 0 || used_ + bytes > kStageCap) begin_stage();
+        int off = used_;
+        used_ += bytes;
+        P.blob.resize((size_t)P.stages[cur_].src_off + used_, 0);
+        return {cur_, off};
+    }
+
+    float* at(int stage, int off) {
+        return reinterpret_cast<float*>(P.blob.data() + P.stages[stage].src_off + off);
+    }
+
+    void close() {
+        if (cur_ >= 0) {
+            P.stages[cur_].bytes = used_;
+            P.stage_max = std::max(P.stage_max, used_);
+        }
+    }
+
+private:
+    Plan& P;
+    int cur_ = -1;
+    int used_ = 0;
+};
+
+void check_net(const df_dense_desc* net, int nd, int in_dim, int out_dim, const char* which) {
+    if (nd < 1) fail(DF_ERR_INVALID, std::string(which) + ": a conditioner needs at least one Dense");
+    if (!net) fail(DF_ERR_INVALID, std::string(which) + ": null Dense array");
+    int prev = in_dim;
+    for (int k = 0; k < nd; ++k) {
+        const df_dense_desc& D = net[k];
+        if (D.in_dim != prev) {
+            std::ostringstream os;
+            os << which << ": Dense " << k + 1 << " expects " << D.in_dim << " inputs but receives " << prev;
+            fail(DF_ERR_SHAPE, os.str());
+        }
+        if (D.out_dim < 1 || !D.W) fail(DF_ERR_INVALID, std::string(which) + ": empty Dense");
+        if (D.act < DF_ACT_IDENTITY || D.act > DF_ACT_SWISH)
+            fail(DF_ERR_INVALID, std::string(which) + ": unknown activation");
+        if (k + 1 < nd && D.out_dim > kMaxHidden) fail(DF_ERR_UNSUPPORTED, "hidden width > 256");
+        prev = D.out_dim;
+    }
+    if (prev != out_dim) {
+        std::ostringstream os;
+        os << which << ": output dimension " << prev << " does not match the " << out_dim
+           << " transformed dimensions";
+        fail(DF_ERR_SHAPE, os.str());
+    }
+}
+
+}  // namespace
+
+size_t plan_lds_bytes(const Plan& p) {
+    size_t tab = (size_t)round_up((int)p.tables.size() * 4, 16);
+    return (size_t)p.stage_max + tab + (size_t)p.samples_per_block * p.stride * 4;
+}
+
+int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
+    try {
+        if (!desc || !out) fail(DF_ERR_INVALID, "null descriptor");
+        if (desc->abi_version != DF_ABI_VERSION) fail(DF_ERR_INVALID, "ABI version mismatch");
+        const int d = desc->d, n = desc->n;
+        if (d < 1 || n < 0) fail(DF_ERR_INVALID, "d must be >= 1 and n >= 0");
+        if (n + d > kMaxState) fail(DF_ERR_UNSUPPORTED, "n + d > 64 is outside the fused kernel's limits");
+        if (desc->n_layers < 1 || !desc->layers) fail(DF_ERR_INVALID, "a FlowChain needs at least one element");
+        if (desc->n_layers > kMaxLayers) fail(DF_ERR_UNSUPPORTED, "too many layers");
+
+        Plan P;
+        P.d = d;
+        P.n = n;
+        P.n_layers = desc->n_layers;
+        P.stride = n + d + 1;                 // [θ | z | 0]
+        if (P.stride % 2 == 0) P.stride += 1; // odd stride: spread LDS banks
+
+        // ---------- pass 0: output path of the conditioner nets ----------
+        // A final Dense with <= 4 outputs after >= 1 hidden Dense is evaluated as a
+        // VALU GEMV (kernel variant OUTV); the choice is chain-wide.
+        bool all_valu = true;
+        for (int li = 0; li < desc->n_layers; ++li) {
+            const df_layer_desc& L = desc->layers[li];
+            if (L.kind == DF_LAYER_NORM) continue;
+            const bool ok = (L.kind == DF_LAYER_NICE || L.n_dense_s >= 2) && L.n_dense_t >= 2 && L.n_af <= 4;
+            all_valu = all_valu && ok;
+        }
+        P.outv = all_valu ? 1 : 0;
+
+        // ---------- pass 1: validation, kernel variant (row tiles) ----------
+        int max_tiles = 1;
+        for (int li = 0; li < desc->n_layers; ++li) {
+            const df_layer_desc& L = desc->layers[li];
+            if (li > 0 && L.element < desc->layers[li - 1].element)
+                fail(DF_ERR_INVALID, "layer element indices must be non-decreasing");
+            if (L.kind == DF_LAYER_NORM) {
+                if (!L.x_min || !L.x_max) fail(DF_ERR_INVALID, "NormalizationLayer without x_min/x_max");
+                if (!(L.beta > L.alpha))
+                    fail(DF_ERR_INVALID, "Bounds of the normalisation need to be in the correct order, β > α.");
+                continue;
+            }
+            if (L.kind != DF_LAYER_RNVP && L.kind != DF_LAYER_NICE) fail(DF_ERR_INVALID, "unknown layer kind");
+            if (L.n_af < 1 || L.n_af > d || !L.axis_af) fail(DF_ERR_INVALID, "invalid axis_af");
+            if (L.n_af > kMaxAf) fail(DF_ERR_UNSUPPORTED, "more than 32 transformed dims in one layer");
+            std::set<int> seen;
+            for (int k = 0; k < L.n_af; ++k) {
+                int a = L.axis_af[k];
+                if (a < 1 || a > d) fail(DF_ERR_INVALID, "The mask cannot contain values higher than the dimension");
+                if (!seen.insert(a).second) fail(DF_ERR_INVALID, "axis_af contains a repeated dimension");
+            }
+            if (L.n_nn < 1 || L.n_nn > n + d || !L.axis_nn) fail(DF_ERR_INVALID, "invalid axis_nn");
+            for (int k = 0; k < L.n_nn; ++k) {
+                if (L.axis_nn[k] < 1 || L.axis_nn[k] > n + d) fail(DF_ERR_INVALID, "axis_nn out of range");
+                // the conditioner must not read transformed dims (else the layer is not a coupling)
+                if (L.axis_nn[k] > n && seen.count(L.axis_nn[k] - n))
+                    fail(DF_ERR_UNSUPPORTED, "axis_nn contains a transformed dimension");
+            }
+            if (L.kind == DF_LAYER_RNVP) {
+                check_net(L.s_net, L.n_dense_s, L.n_nn, L.n_af, "s_net");
+            } else if (L.n_dense_s != 0) {
+                fail(DF_ERR_INVALID, "NICECouplingLayer has no s_net");
+            }
+            check_net(L.t_net, L.n_dense_t, L.n_nn, L.n_af, "t_net");
+            auto scan = [&](const df_dense_desc* net, int nd) {
+                for (int k = 0; k < nd; ++k) {
+                    bool last = (k + 1 == nd);
+                    bool valu_last = last && all_valu;
+                    if (!valu_last) max_tiles = std::max(max_tiles, (net[k].out_dim + 15) / 16);
+                    if (k > 0) max_tiles = std::max(max_tiles, (net[k].in_dim + 15) / 16);
+                }
+            };
+            if (L.kind == DF_LAYER_RNVP) scan(L.s_net, L.n_dense_s);
+            scan(L.t_net, L.n_dense_t);
+        }
+        P.ht = pow2_tiles(max_tiles);
+        if (P.ht > kMaxHidden / 16) fail(DF_ERR_UNSUPPORTED, "hidden width > 256");
+        P.tiles = P.ht <= 4 ? kTilesSmall : 1;
+        P.samples_per_block = kWavesPerBlock * 16 * P.tiles;
+
+        // ---------- pass 2: packing ----------
+        Packer pk(P);
+        const int zero_slot = n + d;
+        for (int li = 0; li < desc->n_layers; ++li) {
+            const df_layer_desc& L = desc->layers[li];
+            DevLayer DL{};
+            DL.kind = L.kind;
+            DL.elem_start = (li == 0 || desc->layers[li - 1].element != L.element) ? 1 : 0;
+            DL.elem_end = (li + 1 == desc->n_layers || desc->layers[li + 1].element != L.element) ? 1 : 0;
+
+            if (L.kind == DF_LAYER_NORM) {
+                DL.norm_off = (int)P.params.size();
+                for (int i = 0; i < d; ++i) P.params.push_back(L.x_min[i]);
+                for (int i = 0; i < d; ++i) P.params.push_back(L.x_max[i]);
+                DL.alpha = L.alpha;
+                DL.beta = L.beta;
+                // ldj = sum(log.(x_diff ./ δ)) in Float32, sequential (Base.sum, n < 16)
+                // src/norm/Normalization.jl:88
+                const float delta = L.beta - L.alpha;
+                float acc = 0.f;
+                for (int i = 0; i < d; ++i) {
+                    float xd = L.x_max[i] - L.x_min[i];
+                    float v = logf(xd / delta);
+                    acc = (i == 0) ? v : acc + v;
+                }
+                DL.ldj_const = acc;
+                P.layers.push_back(DL);
+                continue;
+            }
+
+            DL.n_af = L.n_af;
+            const int ks_state = (L.n_nn + 3) / 4;
+            // feature table [ks*4]: k = 4s + g → state slot of vcat(θ,z)[axis_nn[k]]
+            DL.feat_tab = (int)P.tables.size();
+            for (int k = 0; k < ks_state * 4; ++k)
+                P.tables.push_back(k < L.n_nn ? L.axis_nn[k] - 1 : zero_slot);
+            DL.af_tab = (int)P.tables.size();
+            for (int k = 0; k < L.n_af; ++k) P.tables.push_back(n + L.axis_af[k] - 1);
+
+            const bool valu = all_valu;
+            DL.out_valu = valu ? 1 : 0;
+
+            // Create DevDense entries and the item list for this layer.
+            std::vector<Item> items;
+            auto add_net = [&](const df_dense_desc* net, int nd, int32_t* first, int32_t* count) {
+                *first = (int)P.denses.size();
+                *count = nd;
+                int prev_tiles = 0;
+                for (int k = 0; k < nd; ++k) {
+                    const df_dense_desc& D = net[k];
+                    DevDense DD{};
+                    DD.in_kind = (k == 0) ? IN_STATE : IN_HIDDEN;
+                    DD.n_out = D.out_dim;
+                    DD.act = D.act;
+                    DD.has_bias = D.b ? 1 : 0;
+                    DD.out_valu = (k + 1 == nd) && valu ? 1 : 0;
+                    if (DD.in_kind == IN_STATE) {
+                        DD.ks = ks_state;
+                        DD.kt_in = 0;
+                    } else {
+                        DD.kt_in = prev_tiles;
+                        DD.ks = 4 * prev_tiles;
+                    }
+                    DD.mt = DD.out_valu ? 0 : (D.out_dim + 15) / 16;
+                    prev_tiles = DD.mt;
+                    int idx = (int)P.denses.size();
+                    P.denses.push_back(DD);
+                    if (DD.out_valu) {
+                        items.push_back({Item::W3, idx, 0, round_up((D.out_dim * 16 * DD.kt_in + 4) * 4, 16)});
+                    } else {
+                        int nkq = (DD.ks + 3) / 4;
+                        for (int kq = 0; kq < nkq; ++kq) items.push_back({Item::CHUNK_KQ, idx, kq, DD.mt * 1024});
+                        items.push_back({Item::BIAS, idx, 0, DD.mt * 16 * 4});
+                    }
+                }
+            };
+            if (L.kind == DF_LAYER_RNVP) add_net(L.s_net, L.n_dense_s, &DL.s_dense0, &DL.s_ndense);
+            else { DL.s_dense0 = 0; DL.s_ndense = 0; }
+            add_net(L.t_net, L.n_dense_t, &DL.t_dense0, &DL.t_ndense);
+
+            // Keep a layer inside one stage whenever it fits.
+            int layer_bytes = 0;
+            for (auto& it : items) layer_bytes += it.bytes;
+            if (layer_bytes > pk.remaining()) pk.begin_stage();
+
+            // dense index → source Dense for packing
+            auto src_of = [&](int dense_idx) -> const df_dense_desc& {
+                if (L.kind == DF_LAYER_RNVP && dense_idx < DL.s_dense0 + DL.s_ndense)
+                    return L.s_net[dense_idx - DL.s_dense0];
+                return L.t_net[dense_idx - DL.t_dense0];
+            };
+
+            for (auto& it : items) {
+                DevDense& DD = P.denses[it.dense];
+                const df_dense_desc& D = src_of(it.dense);
+                const int out = D.out_dim, in = D.in_dim;
+                auto W = [&](int row, int k) -> float {
+                    return (row < out && k < in) ? D.W[(size_t)row + (size_t)out * k] : 0.f;
+                };
+                auto [st, off] = pk.alloc(it.bytes);
+                float* dst = pk.at(st, off);
+                if (it.kind == Item::CHUNK_KQ) {
+                    // merge with the previous chunk of this dense when contiguous in the same stage
+                    if (DD.n_chunks > 0) {
+                        DevChunk& C = P.chunks[DD.chunk0 + DD.n_chunks - 1];
+                        if (C.stage == st && C.lds_off + (C.kq_end - C.kq_begin) * DD.mt * 1024 == off &&
+                            C.kq_end == it.kq) {
+                            C.kq_end++;
+                        } else {
+                            P.chunks.push_back({st, off, it.kq, it.kq + 1});
+                            DD.n_chunks++;
+                        }
+                    } else {
+                        DD.chunk0 = (int)P.chunks.size();
+                        P.chunks.push_back({st, off, it.kq, it.kq + 1});
+                        DD.n_chunks = 1;
+                    }
+                    // fragment [m][lane][r] for k-quad kq
+                    for (int m = 0; m < DD.mt; ++m)
+                        for (int lane = 0; lane < 64; ++lane)
+                            for (int r = 0; r < 4; ++r) {
+                                const int i = lane & 15, g = lane >> 4;
+                                const int s = 4 * it.kq + r;
+                                const int row = 16 * m + i;
+                                int k;
+                                if (DD.in_kind == IN_STATE) k = (s < DD.ks) ? 4 * s + g : in;  // beyond in → 0
+                                else k = 16 * it.kq + 4 * g + r;
+                                dst[(m * 64 + lane) * 4 + r] = W(row, k);
+                            }
+                } else if (it.kind == Item::BIAS) {
+                    DD.bias_stage = st;
+                    DD.bias_lds = off;
+                    for (int row = 0; row < DD.mt * 16; ++row)
+                        dst[row] = (D.b && row < out) ? D.b[row] : 0.f;
+                } else {  // W3: VALU GEMV output  [o][16*kt_in] then b[4]
+                    DD.w3_stage = st;
+                    DD.w3_lds = off;
+                    const int inp = 16 * DD.kt_in;
+                    for (int o = 0; o < out; ++o)
+                        for (int k = 0; k < inp; ++k) dst[o * inp + k] = W(o, k);
+                    for (int o = 0; o < 4; ++o) dst[out * inp + o] = (D.b && o < out) ? D.b[o] : 0.f;
+                }
+                (void)in;
+            }
+            P.layers.push_back(DL);
+
+            // bookkeeping: parameters and algorithmic FLOPs (2 × MACs)
+            auto count = [&](const df_dense_desc* net, int nd) {
+                for (int k = 0; k < nd; ++k) {
+                    P.n_params += (int64_t)net[k].in_dim * net[k].out_dim + (net[k].b ? net[k].out_dim : 0);
+                    P.flops_per_sample += 2.0 * net[k].in_dim * net[k].out_dim;
+                }
+            };
+            if (L.kind == DF_LAYER_RNVP) count(L.s_net, L.n_dense_s);
+            count(L.t_net, L.n_dense_t);
+        }
+        pk.close();
+        if ((int)P.tables.size() > kMaxTableInts) fail(DF_ERR_UNSUPPORTED, "chain index tables exceed 16 KiB");
+        if (P.stages.empty()) {  // normalization-only chain: keep one empty stage record
+            P.stage_max = 0;
+        }
+        P.blob.resize(round_up((int)P.blob.size(), 16) + 16, 0);
+        *out = std::move(P);
+        return DF_OK;
+    } catch (const Fail& f) {
+        if (err) *err = f.msg;
+        return f.code;
+    } catch (const std::exception& e) {
+        if (err) *err = e.what();
+        return DF_ERR_INVALID;
+    }
+}
+
+}  // namespace df

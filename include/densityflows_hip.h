@@ -1,0 +1,197 @@
+/*
+ * densityflows_hip.h — C ABI of the MI355X-native DensityFlows.jl hot path.
+ *
+ * The library (libdensityflows_hip.so, built for gfx950) evaluates a
+ * DensityFlows.jl `FlowChain` of RealNVP / NICE coupling layers, coupling
+ * blocks and NormalizationLayers over a batch of samples with fused HIP
+ * kernels: the s/t conditioner MLPs run on f32 MFMA, the coupling transform,
+ * the per-layer log-det-Jacobian (ldj) accumulation and the base-density
+ * logpdf are fused behind them.
+ *
+ * Every entry point below replaces one Julia method of the reference
+ * (DensityFlows.jl v1.0.0).  A Julia front-end binds them with `ccall`
+ * (see INTEGRATION.md and densityflows.jl_amd/julia/DensityFlowsHIP.jl);
+ * the Python host mirror binds them with ctypes.
+ *
+ * Conventions
+ * -----------
+ *  - Memory layout is exactly Julia's: a (d, B) Float32 matrix is
+ *    column-major, so sample j occupies x[d*j .. d*j+d-1].  θ is (n, B), may
+ *    be n = 0 (pointer may then be NULL).  ldj / logpdf are (B,).
+ *  - Dense weights are Flux's `Dense.weight`: an (out, in) column-major
+ *    Float32 matrix (W[i + out*k] = W_ik); `bias` has `out` entries or is
+ *    NULL (`bias=false`).  Axes are Julia's 1-based index vectors.
+ *  - Batch-compute calls take DEVICE pointers and a HIP stream (NULL = the
+ *    default stream) and are stream-ordered (asynchronous w.r.t. the host).
+ *  - All functions return DF_OK (0) or a negative df_status; the message of
+ *    the last error on the calling thread is returned by df_last_error().
+ *  - A df_chain handle is bound to one device and is not thread-safe;
+ *    different handles may be used concurrently.
+ */
+#ifndef DENSITYFLOWS_HIP_H
+#define DENSITYFLOWS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DF_ABI_VERSION 1
+
+typedef enum df_status {
+    DF_OK = 0,
+    DF_ERR_INVALID = -1,     /* malformed descriptor / argument (Julia: ArgumentError) */
+    DF_ERR_SHAPE = -2,       /* shape or rank mismatch (Julia: AssertionError / DimensionMismatch) */
+    DF_ERR_HIP = -3,         /* HIP runtime error */
+    DF_ERR_UNSUPPORTED = -4, /* structure outside the kernel's limits (see df_limits) */
+    DF_ERR_NOMEM = -5,       /* device allocation failed */
+    DF_ERR_NONFINITE = -6    /* a NaN/Inf was found where the caller asked for a check */
+} df_status;
+
+/* Activation functions σ of Flux.Dense (NNlib definitions). */
+typedef enum df_act {
+    DF_ACT_IDENTITY = 0,
+    DF_ACT_RELU = 1,
+    DF_ACT_TANH = 2,
+    DF_ACT_SIGMOID = 3,
+    DF_ACT_SOFTPLUS = 4,
+    DF_ACT_LOGCOSH = 5,
+    DF_ACT_LEAKYRELU = 6,  /* slope 0.01 */
+    DF_ACT_ELU = 7,        /* α = 1 */
+    DF_ACT_SWISH = 8
+} df_act;
+
+/* FlowElement kinds that the kernels evaluate. */
+typedef enum df_layer_kind {
+    DF_LAYER_RNVP = 0, /* RNVPCouplingLayer  (src/affine/RNVP.jl:41-48)          */
+    DF_LAYER_NICE = 1, /* NICECouplingLayer  (src/affine/NICE.jl:31-36)          */
+    DF_LAYER_NORM = 2  /* NormalizationLayer (src/norm/Normalization.jl:30-35)   */
+} df_layer_kind;
+
+/* One Flux.Dense(in, out, σ; bias).  src/Layers.jl:33-50. */
+typedef struct df_dense_desc {
+    int32_t in_dim;
+    int32_t out_dim;
+    int32_t act;        /* df_act */
+    const float* W;     /* (out, in) column-major, host memory */
+    const float* b;     /* out entries, or NULL for bias=false */
+} df_dense_desc;
+
+/* One flat layer of the chain.  CouplingBlocks (src/Blocks.jl:64-75) are
+ * given as two consecutive layers with the same `element` index; the chain's
+ * ldj is then accumulated exactly as the reference groups it:
+ *   element ldj = ldj_1 .+ ldj_2            (src/Blocks.jl:136,149)
+ *   chain ldj   = ldj_e1 .+ ldj_e2 .+ ...   (src/Chains.jl:160,179)          */
+typedef struct df_layer_desc {
+    int32_t kind;       /* df_layer_kind */
+    int32_t element;    /* index of the FlowElement this layer belongs to */
+    /* coupling layers: CouplingAxes (src/Axes.jl:28-35), 1-based */
+    int32_t n_af;
+    const int32_t* axis_af;  /* transformed dims, user (mask) order      */
+    int32_t n_nn;
+    const int32_t* axis_nn;  /* conditioner input rows of vcat(θ, z)     */
+    int32_t n_dense_s;       /* 0 for NICE */
+    const df_dense_desc* s_net;
+    int32_t n_dense_t;
+    const df_dense_desc* t_net;
+    /* NormalizationLayer fields */
+    const float* x_min;      /* d entries */
+    const float* x_max;      /* d entries */
+    float alpha;
+    float beta;
+} df_layer_desc;
+
+typedef struct df_chain_desc {
+    int32_t abi_version;     /* DF_ABI_VERSION */
+    int32_t d;               /* data dimensions */
+    int32_t n;               /* condition dimensions (0 = unconditional) */
+    int32_t n_layers;
+    const df_layer_desc* layers;
+} df_chain_desc;
+
+/* Structural limits of the fused kernels. */
+typedef struct df_limits {
+    int32_t max_state;       /* n + d                      */
+    int32_t max_hidden;      /* widest hidden Dense        */
+    int32_t max_af;          /* transformed dims per layer */
+    int32_t max_layers;
+} df_limits;
+
+typedef struct df_chain_info {
+    int32_t d, n, n_layers;
+    int32_t hidden_tiles;         /* kernel variant: padded hidden width / 16 */
+    int32_t samples_per_block;    /* samples one workgroup processes          */
+    int32_t n_stages;             /* LDS weight stages per chain pass         */
+    int64_t n_params;             /* trainable parameters (Flux.trainables)   */
+    double flops_per_sample;      /* 2 × Σ Dense MACs (algorithmic)           */
+    int64_t weight_bytes;         /* packed device weight blob                */
+} df_chain_info;
+
+int df_get_abi_version(void);
+const char* df_last_error(void);
+int df_get_limits(df_limits* out);
+
+/* ---- chain lifetime ------------------------------------------------------ */
+
+typedef struct df_chain df_chain;
+
+/* Validate and plan a descriptor without touching a device (the same checks
+ * df_chain_create performs); fills `info` when non-NULL. */
+int df_chain_validate(const df_chain_desc* desc, df_chain_info* info);
+
+/* Build a device-resident chain (weights are copied and re-laid-out into MFMA
+ * fragment order).  Replaces the Julia-side `FlowChain` object
+ * (src/Chains.jl:78-80) for evaluation.  `device` = HIP device ordinal. */
+int df_chain_create(df_chain** out, const df_chain_desc* desc, int device);
+int df_chain_destroy(df_chain* chain);
+int df_chain_get_info(const df_chain* chain, df_chain_info* out);
+
+/* θ bounds of the Flow's MetaData (src/Data.jl:75-86; n floats each, host
+ * memory).  Enables the df_flow_* entry points' in-kernel θ normalisation. */
+int df_chain_set_theta_bounds(df_chain* chain, const float* theta_min, const float* theta_max);
+
+/* ---- chain level (θ used as given) ---------------------------------------
+ * forward(chain, z, θ)  -> (x, ldj)      src/Chains.jl:168-184
+ * backward(chain, x, θ) -> (z, ldj)      src/Chains.jl:149-165
+ * forward!(chain, z, θ)                  src/Chains.jl:187-197  (in place, no ldj)
+ * `ldj` may be NULL (not written).  `x_out` may alias `z` for forward. */
+int df_chain_forward(df_chain* chain, const float* z, const float* theta,
+                     float* x_out, float* ldj_out, int64_t batch, void* stream);
+int df_chain_backward(df_chain* chain, const float* x, const float* theta,
+                      float* z_out, float* ldj_out, int64_t batch, void* stream);
+int df_chain_forward_inplace(df_chain* chain, float* z, const float* theta,
+                             int64_t batch, void* stream);
+
+/* ---- flow level (θ raw, normalised in-kernel with the stored bounds) -----
+ * The @flow_wrapper methods (src/Macros.jl:104-112, applied at
+ * src/DensityFlows.jl:72): f(flow, y, θ) = f(flow.model, y, normalize_input(θ)).
+ * df_flow_logpdf: src/Flows.jl:272-281 — backward pass + MvNormal(0, I)
+ * log-density + ldj, written per sample.
+ * df_flow_logpdf_sum: Σ_j logpdf_j accumulated in fp64, deterministic
+ * order, written to ONE double in device memory (the NLL partial that
+ * src/Flows.jl:352-359 averages; all-reduced across GPUs by the caller). */
+int df_flow_forward(df_chain* chain, const float* z, const float* theta_raw,
+                    float* x_out, float* ldj_out, int64_t batch, void* stream);
+int df_flow_backward(df_chain* chain, const float* x, const float* theta_raw,
+                     float* z_out, float* ldj_out, int64_t batch, void* stream);
+int df_flow_forward_inplace(df_chain* chain, float* z, const float* theta_raw,
+                            int64_t batch, void* stream);
+int df_flow_logpdf(df_chain* chain, const float* x, const float* theta_raw,
+                   float* logpdf_out, int64_t batch, void* stream);
+int df_flow_logpdf_sum(df_chain* chain, const float* x, const float* theta_raw,
+                       double* sum_out, int64_t batch, void* stream);
+
+/* ---- device memory helpers (for hosts without a GPU array package) ------ */
+int df_device_alloc(void** ptr, size_t bytes);
+int df_device_free(void* ptr);
+int df_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int df_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int df_stream_synchronize(void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DENSITYFLOWS_HIP_H */

@@ -1,0 +1,251 @@
+"""GPU parity: the fused HIP path (through the C ABI) against the CPU oracle
+and the committed golden fixtures.
+
+Criterion (BASELINE.json north_star): 1e-5 relative fp32 tolerance, with an
+absolute floor of 1e-5 × max|expected| (helpers.close); bit-exact for
+index/mask selection (identity dims are copied, never recomputed) and exact
+forward/inverse ldj cancellation per layer (test/runtests.jl:54,62).
+"""
+import numpy as np
+import pytest
+
+import densityflows_amd as dfa
+import make_golden as G
+from helpers import close, spec_to_element
+from oracle import flow_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def _t(a, dev):
+    """numpy (rows, B) → Julia-layout (column-major) device tensor."""
+    import torch
+
+    a = np.asarray(a, np.float32)
+    return torch.from_numpy(np.ascontiguousarray(a.T)).to(dev).T
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4"])
+def test_golden_forward_backward(cuda, name):
+    spec, g, meta = G.load(name)
+    chain = spec_to_element(spec)
+    th = _t(g["theta"], cuda) if meta["n"] > 0 else None
+    x, lf = dfa.forward(chain, _t(g["z"], cuda), th)
+    ok, r = close(_np(x), g["x_fwd"], RTOL)
+    assert ok, f"forward x ratio {r}"
+    ok, r = close(_np(lf), g["ldj_fwd"], RTOL)
+    assert ok, f"forward ldj ratio {r}"
+    z, lb = dfa.backward(chain, _t(g["x_in"], cuda), th)
+    ok, r = close(_np(z), g["z_bwd"], RTOL)
+    assert ok, f"backward z ratio {r}"
+    ok, r = close(_np(lb), g["ldj_bwd"], RTOL)
+    assert ok, f"backward ldj ratio {r}"
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4"])
+def test_identity_dims_bit_exact(cuda, name):
+    """Dims a layer does not transform are copied bit for bit: with a single
+    coupling layer the identity rows of x equal z exactly."""
+    spec, g, meta = G.load(name)
+    first = spec["layers"][0]
+    layer = first["layer_1"] if first["kind"] == "block" else first
+    el = spec_to_element(layer)
+    th = _t(g["theta"], cuda) if meta["n"] > 0 else None
+    x, _ = dfa.forward(el, _t(g["z"], cuda), th)
+    idx = np.asarray(layer["axis_id"]) - 1
+    np.testing.assert_array_equal(_np(x)[idx], g["z"][idx])
+
+
+@pytest.mark.parametrize("mask", [None, [1, 3, 5, 7], [4, 2, 5, 1, 6]])
+def test_runtests_real_nvp(cuda, mask):
+    """test/runtests.jl:43-64 on the GPU path: round trip and EXACT ldj cancellation."""
+    rng = np.random.default_rng(5)
+    layer = (dfa.CouplingLayer(dfa.RNVPCouplingLayer, 7, 3, n=2, rng=rng) if mask is None
+             else dfa.CouplingLayer(dfa.RNVPCouplingLayer, 7, mask, n=2, rng=rng))
+    z1 = np.full((7, 10), 0.2, np.float32)
+    th = np.full((2, 10), 0.1, np.float32)
+    x, l1 = dfa.forward(layer, _t(z1, cuda), _t(th, cuda))
+    z2, l2 = dfa.backward(layer, x, _t(th, cuda))
+    np.testing.assert_allclose(_np(z2), z1, rtol=np.sqrt(np.finfo(np.float32).eps))
+    assert np.all(_np(l1) + _np(l2) == 0)
+    # and against the oracle
+    xo, lo = O.forward(layer.to_spec(), z1, th, np.float64)
+    assert close(_np(x), xo, RTOL)[0] and close(_np(l1), lo, RTOL)[0]
+
+
+def test_runtests_chain(cuda):
+    """test/runtests.jl:66-95: mixed chain (unsorted masks, block, NormalizationLayer)."""
+    rng = np.random.default_rng(6)
+    layer_1 = dfa.CouplingLayer(dfa.RNVPCouplingLayer, 7, [1, 3, 5, 7], n=2, rng=rng)
+    layer_2 = dfa.CouplingLayer(dfa.RNVPCouplingLayer, 7, [4, 2, 5, 1, 6], n=2, rng=rng)
+    block = dfa.CouplingBlock.build(7, [4, 2, 5, 1], n=2, rng=rng)
+    small = dfa.FlowChain(layer_1, layer_2)
+    assert len(dfa.concatenate(small, block)) == 3
+    assert len(dfa.concatenate(block, small)) == 3
+    x1 = np.full((7, 10), 0.2, np.float32)
+    th = np.full((2, 10), 0.1, np.float32)
+    x1[:, 1] = 0.4
+    th[0, 1] = 0.4
+    chain = dfa.concatenate((small, dfa.FlowChain(block, dfa.NormalizationLayer.from_data(x1))))
+    assert isinstance(chain[-1], dfa.NormalizationLayer)
+    z, lb = dfa.backward(chain, _t(x1, cuda), _t(th, cuda))
+    x2, lf = dfa.forward(chain, z, _t(th, cuda))
+    np.testing.assert_allclose(_np(x2), x1, rtol=np.sqrt(np.finfo(np.float32).eps), atol=1e-6)
+    assert np.all(np.abs(_np(lf) + _np(lb)) <= 2e-6)
+    zo, lbo = O.backward(chain.to_spec(), x1, th, np.float64)
+    assert close(_np(z), zo, RTOL)[0] and close(_np(lb), lbo, RTOL)[0]
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2"])
+def test_flow_level_theta_normalisation_and_logpdf(cuda, name):
+    """@flow_wrapper (θ normalised in-kernel) and fused logpdf / logpdf_sum."""
+    spec, g, meta = G.load(name)
+    chain = spec_to_element(spec)
+    md = dfa.MetaData("", meta["d"], meta["n"], g["theta_min"], g["theta_max"])
+    flow = dfa.Flow(chain, metadata=md)
+    th_raw = _t(g["theta_raw"], cuda) if meta["n"] > 0 else None
+    x, lf = flow.forward(_t(g["z"], cuda), th_raw)
+    assert close(_np(x), g["x_fwd"], RTOL)[0] and close(_np(lf), g["ldj_fwd"], RTOL)[0]
+    lp = dfa.logpdf(flow, _t(g["x_in"], cuda), th_raw)
+    ok, r = close(_np(lp), g["logpdf"], RTOL)
+    assert ok, r
+    s, cnt = dfa.nll_partial_sum(flow, _t(g["x_in"], cuda), th_raw)
+    assert cnt == meta["B"]
+    assert abs(float(s.item()) - float(np.sum(_np(lp).astype(np.float64)))) <= 1e-9 * meta["B"] * 10
+    assert abs(float(s.item()) - float(np.sum(g["logpdf"]))) <= 1e-5 * np.sum(np.abs(g["logpdf"]))
+
+
+def test_forward_inplace_matches_forward(cuda):
+    spec, g, _ = G.load("cfg2")
+    chain = spec_to_element(spec)
+    x, _ = dfa.forward(chain, _t(g["z"], cuda))
+    zz = _t(g["z"], cuda)
+    dfa.forward_(chain, zz)
+    np.testing.assert_array_equal(_np(zz), _np(x))
+
+
+@pytest.mark.parametrize("B", [0, 1, 7, 127, 128, 129, 1000, 4097])
+def test_ragged_batches(cuda, B):
+    spec, g, _ = G.load("cfg1")
+    chain = spec_to_element(spec)
+    z = g["z"][:, :B]
+    th = g["theta"][:, :B]
+    x, l = dfa.forward(chain, _t(z, cuda), _t(th, cuda))
+    assert tuple(x.shape) == (5, B) and tuple(l.shape) == (B,)
+    if B:
+        assert close(_np(x), g["x_fwd"][:, :B], RTOL)[0]
+        assert close(_np(l), g["ldj_fwd"][:B], RTOL)[0]
+
+
+def test_nd_dims_and_numpy_io(cuda):
+    """(d, dims...) arrays: ldj has shape dims (RNVP.jl:180 dropdims)."""
+    spec, g, _ = G.load("cfg2")
+    chain = spec_to_element(spec)
+    z = g["z"][:, :70].reshape(5, 2, 5, 7, order="F")
+    x, l = dfa.forward(chain, z)          # numpy in → numpy out
+    assert x.shape == (5, 2, 5, 7) and l.shape == (2, 5, 7)
+    assert close(x.reshape(5, 70, order="F"), g["x_fwd"][:, :70], RTOL)[0]
+    assert close(l.reshape(70, order="F"), g["ldj_fwd"][:70], RTOL)[0]
+
+
+@pytest.mark.parametrize("act", ["tanh", "sigmoid", "softplus", "logcosh", "leakyrelu", "elu", "swish", "identity"])
+def test_activations(cuda, act):
+    rng = np.random.default_rng(7)
+    ch = dfa.FlowChain(dfa.CouplingLayer(5, [2, 4], hidden_dim=32, σ=act, rng=rng),
+                       dfa.CouplingLayer(5, [1, 3, 5], hidden_dim=32, σ=act, rng=rng))
+    z = rng.standard_normal((5, 300)).astype(np.float32)
+    x, l = dfa.forward(ch, _t(z, cuda))
+    xo, lo = O.forward(ch.to_spec(), z, np.zeros((0, 300)), np.float64)
+    assert close(_np(x), xo, RTOL)[0] and close(_np(l), lo, RTOL)[0]
+
+
+def test_nice_and_custom_nets(cuda):
+    """NICE layers and hand-built conditioners of mixed widths (docs/src/documentation.md:99-105)."""
+    rng = np.random.default_rng(8)
+    d, n = 7, 1
+    s_net = dfa.Chain([dfa.Dense.init(5, 32, "sigmoid", rng=rng), dfa.Dense.init(32, 16, "relu", rng=rng),
+                       dfa.Dense.init(16, 3, rng=rng)])
+    t_net = dfa.Chain([dfa.Dense.init(5, 12, "relu", rng=rng), dfa.Dense.init(12, 16, "logcosh", rng=rng),
+                       dfa.Dense.init(16, 32, "relu", rng=rng), dfa.Dense.init(32, 3, rng=rng)])
+    ax = dfa.CouplingAxes.from_mask(d, [6, 2, 4], n=n)
+    rn = dfa.CouplingLayer(s_net, t_net, ax)
+    nice = dfa.CouplingLayer(dfa.NICECouplingLayer, d, 3, n=n, rng=rng)
+    ch = dfa.FlowChain(rn, nice, dfa.CouplingBlock.build(d, 4, n=n, rng=rng, hidden_dim=48))
+    z = rng.standard_normal((d, 513)).astype(np.float32)
+    th = rng.random((n, 513)).astype(np.float32)
+    x, l = dfa.forward(ch, _t(z, cuda), _t(th, cuda))
+    xo, lo = O.forward(ch.to_spec(), z, th, np.float64)
+    assert close(_np(x), xo, RTOL)[0] and close(_np(l), lo, RTOL)[0]
+    zb, lb = dfa.backward(ch, x, _t(th, cuda))
+    assert close(_np(zb), z, RTOL)[0]
+    assert np.all(np.abs(_np(l) + _np(lb)) <= 1e-5 * np.maximum(1, np.abs(_np(l))))
+
+
+def test_wide_af_mfma_output_path(cuda):
+    """More than 4 transformed dims → the MFMA output path (n_af up to 32)."""
+    rng = np.random.default_rng(9)
+    ch = dfa.FlowChain.repeat(dfa.CouplingBlock, 2, 40, 20, n=3, hidden_dim_s=64, hidden_dim_t=64, rng=rng)
+    z = rng.standard_normal((40, 777)).astype(np.float32)
+    th = rng.random((3, 777)).astype(np.float32)
+    x, l = dfa.forward(ch, _t(z, cuda), _t(th, cuda))
+    xo, lo = O.forward(ch.to_spec(), z, th, np.float64)
+    assert close(_np(x), xo, RTOL)[0] and close(_np(l), lo, RTOL)[0]
+
+
+def test_full_size_roundtrip_properties(cuda):
+    """BASELINE config 2 at its full size (B = 2^20): size-independent
+    properties — inverse(forward(z)) ≈ z, ldj_f + ldj_b ≈ 0, finite, and a
+    sampled subset against the oracle."""
+    import torch
+
+    spec, _, _ = G.load("cfg2")
+    chain = spec_to_element(spec)
+    B = 1 << 20
+    gen = torch.Generator(device=cuda).manual_seed(1)
+    z = torch.randn(B, 5, device=cuda, generator=gen).T
+    x, lf = dfa.forward(chain, z)
+    zb, lb = dfa.backward(chain, x)
+    assert torch.isfinite(x).all() and torch.isfinite(lf).all()
+    err = (zb - z).abs().max().item()
+    assert err <= 1e-4, err
+    assert (lf + lb).abs().max().item() <= 1e-5
+    idx = torch.randint(0, B, (2048,), device=cuda, generator=gen)
+    zs = _np(z[:, idx])
+    xo, lo = O.forward(spec, zs, np.zeros((0, zs.shape[1])), np.float64)
+    assert close(_np(x[:, idx]), xo, RTOL)[0] and close(_np(lf[idx]), lo, RTOL)[0]
+
+
+def test_deterministic_repeat(cuda):
+    spec, g, _ = G.load("cfg2")
+    chain = spec_to_element(spec)
+    a, la = dfa.forward(chain, _t(g["z"], cuda))
+    b, lb = dfa.forward(chain, _t(g["z"], cuda))
+    np.testing.assert_array_equal(_np(a), _np(b))
+    np.testing.assert_array_equal(_np(la), _np(lb))
+
+
+def test_sample_shape_and_theta_tuple(cuda):
+    """test/runtests.jl:118-120: size(sample(flow, (2,5,7), (-1f0,))) == (5,2,5,7)."""
+    spec, g, meta = G.load("cfg1")
+    md = dfa.MetaData("", 5, 1, g["theta_min"], g["theta_max"])
+    flow = dfa.Flow(spec_to_element(spec), metadata=md)
+    s = dfa.sample(flow, (2, 5, 7), (-1.0,))
+    assert tuple(s.shape) == (5, 2, 5, 7)
+    import torch
+
+    assert torch.isfinite(s).all()
+
+
+def test_errors_are_loud(cuda):
+    spec, g, _ = G.load("cfg1")
+    chain = spec_to_element(spec)
+    with pytest.raises(AssertionError):
+        dfa.forward(chain, _t(g["z"][:4], cuda), _t(g["theta"], cuda))   # wrong d
+    with pytest.raises(AssertionError):
+        dfa.forward(chain, _t(g["z"], cuda), None)                        # missing θ

@@ -1,0 +1,155 @@
+"""Host-side logic on CPU: the C-ABI library loads and exports every symbol the
+header declares; descriptors are validated/planned without a device; the
+Python mirror reproduces the reference's index tables bit for bit."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import densityflows_amd as dfa
+from densityflows_amd import _lib, hip
+from helpers import spec_to_element
+from oracle import flow_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "densityflows_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(df_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_lib.SIGNATURES), "ctypes signatures out of sync with the header"
+    assert lib.df_get_abi_version() == _lib.ABI_VERSION
+
+
+def test_limits():
+    lim = _lib.df_limits()
+    _lib.check(_lib.load().df_get_limits(C.byref(lim)))
+    assert lim.max_state == 64 and lim.max_hidden == 256 and lim.max_af == 32
+
+
+def test_plan_config2_and_config1():
+    rng = np.random.default_rng(0)
+    ch2 = dfa.FlowChain.repeat(dfa.CouplingBlock, 4, 5, hidden_dim_s=64, hidden_dim_t=64, rng=rng)
+    info = hip.validate(ch2.layers)
+    assert info.n_params == 72744 and info.flops_per_sample == 141312.0
+    assert info.hidden_tiles == 4
+    x = np.load(os.path.join(ROOT, "tests", "golden", "datatest_x.npy"))
+    th = np.load(os.path.join(ROOT, "tests", "golden", "datatest_theta.npy"))
+    data = dfa.DataArrays(x, th, rng=rng)
+    ch1 = dfa.FlowChain(*[dfa.CouplingLayer(data, m, hidden_dim_s=16, hidden_dim_t=16, rng=rng)
+                          for m in ([1, 2, 3], [3, 4, 5], [5, 1, 2])],
+                        dfa.NormalizationLayer.from_data(x, -1.0, 1.0))
+    info = hip.validate(ch1.layers)
+    assert info.n_params == 2322 and info.flops_per_sample == 4224.0 and info.n_stages == 1
+
+
+def test_plan_config4():
+    rng = np.random.default_rng(0)
+    ch4 = dfa.FlowChain.repeat(dfa.CouplingBlock, 8, 32, n=8, hidden_dim_s=256, hidden_dim_t=256, rng=rng)
+    info = hip.validate(ch4.layers)
+    assert info.n_params == 2441728 and info.flops_per_sample == 4849664.0
+    assert info.hidden_tiles == 16 and info.n_stages > 16
+
+
+def test_doctest_summaries():
+    # src/Layers.jl:99-104 and src/Blocks.jl:51-59
+    s = dfa.summarize(dfa.CouplingLayer(3, [1, 3], n=2, hidden_dim=10, n_sublayers_s=1, σ="tanh"))
+    assert s.splitlines() == [
+        "RNVPCouplingLayer | s_net > [3, 10, 2] (62 parameters)",
+        "                  | t_net > [3, 10, 10, 2] (172 parameters)",
+        "                  | axes  > (d,n)=(3,2); identity=(2), transformed=(1,3)"]
+    b = dfa.summarize(dfa.CouplingBlock.build(3, [1, 3], n=2, hidden_dim=10, n_sublayers_s=1, σ="tanh"))
+    assert b.splitlines()[3:] == [
+        "RNVPCouplingLayer | s_net > [4, 10, 1] (61 parameters)",
+        "                  | t_net > [4, 10, 10, 1] (171 parameters)",
+        "                  | axes  > (d,n)=(3,2); identity=(1,3), transformed=(2)"]
+
+
+@pytest.mark.parametrize("mask", [[1, 2, 3], [5, 1, 2], [4, 2, 5, 1, 6], [3]])
+def test_axes_tables_match_oracle(mask):
+    d = max(6, max(mask))
+    a = dfa.CouplingAxes.from_mask(d, mask, n=2)
+    o = O.coupling_axes(d, mask, n=2)
+    assert (a.axis_id, a.axis_af, a.axis_nn) == (o["axis_id"], o["axis_af"], o["axis_nn"])
+    r, ro = dfa.reverse(a), O.reverse_axes(o)
+    assert (r.axis_id, r.axis_af, r.axis_nn) == (ro["axis_id"], ro["axis_af"], ro["axis_nn"])
+    assert dfa.is_reverse(a, r)
+
+
+def test_axes_equality_runtests():
+    data = dfa.DataArrays(np.ones((7, 10), np.float32), np.ones((2, 10), np.float32))
+    from densityflows_amd.axes import CouplingAxes_
+    ref = dfa.CouplingAxes.from_cut(7, 3, n=2)
+    assert dfa.CouplingAxes.from_mask(7, [4, 5, 6, 7], n=2) == ref
+    assert CouplingAxes_(data) == ref
+    assert CouplingAxes_(data, [4, 5, 6, 7]) == ref
+    assert CouplingAxes_(data, 3) == ref
+
+
+def test_spec_roundtrip():
+    rng = np.random.default_rng(1)
+    ch = dfa.FlowChain(dfa.CouplingLayer(5, [2, 4], n=1, rng=rng), dfa.CouplingBlock.build(5, 2, n=1, rng=rng))
+    again = spec_to_element(ch.to_spec())
+    assert again.num_params() == ch.num_params()
+    np.testing.assert_array_equal(again[0].s_net[0].W, ch[0].s_net[0].W)
+
+
+def test_validation_errors_map_to_reference_exceptions():
+    rng = np.random.default_rng(2)
+    # NormalizationLayer β ≤ α  (Normalization.jl:55)
+    with pytest.raises(AssertionError):
+        dfa.NormalizationLayer(np.zeros(3), np.ones(3), 1.0, 0.0)
+    # CouplingBlock with non-complementary axes (Blocks.jl:71)
+    l1 = dfa.CouplingLayer(5, [1, 2], rng=rng)
+    l2 = dfa.CouplingLayer(5, [3, 4], rng=rng)
+    with pytest.raises(dfa.ArgumentError):
+        dfa.CouplingBlock(l1, l2)
+    # mask beyond d (Axes.jl:85)
+    with pytest.raises(AssertionError):
+        dfa.CouplingAxes.from_mask(3, [4])
+    # mixed d in one chain
+    with pytest.raises(AssertionError):
+        hip.validate([dfa.CouplingLayer(5, [1], rng=rng), dfa.CouplingLayer(6, [1], rng=rng)])
+    # hidden width beyond the kernel limit
+    with pytest.raises(dfa.UnsupportedError):
+        hip.validate([dfa.CouplingLayer(5, [1], hidden_dim=300, rng=rng)])
+
+
+def test_c_abi_rejects_bad_descriptor_without_device():
+    lib = _lib.load()
+    desc = _lib.df_chain_desc(_lib.ABI_VERSION + 7, 5, 0, 0, None)
+    assert lib.df_chain_validate(C.byref(desc), None) == _lib.DF_ERR_INVALID
+    assert b"ABI" in lib.df_last_error()
+    desc = _lib.df_chain_desc(_lib.ABI_VERSION, 70, 0, 1, None)
+    assert lib.df_chain_validate(C.byref(desc), None) == _lib.DF_ERR_UNSUPPORTED
+
+
+def test_product_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "densityflows.jl_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h", ".jl")):
+                src = open(os.path.join(dirpath, f), encoding="utf-8").read()
+                assert "flow_oracle" not in src and "oracle/" not in src, f
+
+
+def test_no_gpu_means_loud_failure():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    rng = np.random.default_rng(3)
+    ch = dfa.FlowChain(dfa.CouplingLayer(5, [1, 2], rng=rng))
+    with pytest.raises(dfa.HIPError):
+        dfa.forward(ch, np.zeros((5, 4), np.float32))

@@ -1,0 +1,143 @@
+"""Pin the CPU oracle against everything the reference's own tests hold
+(test/runtests.jl, doctests) and against the committed golden fixtures.
+CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+import make_golden as G
+from helpers import close
+from oracle import flow_oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+# --- test/runtests.jl:33-41 ("axes") ----------------------------------------
+def test_axes_equalities():
+    a = O.coupling_axes(7, [4, 5, 6, 7], n=2)
+    b = O.coupling_axes_cut(7, 3, n=2)
+    assert O.axes_equal(a, b)
+    # data constructors give the same (d=7, n=2 from the data shape)
+    assert O.axes_equal(O.coupling_axes_cut(7, 7 // 2, n=2), b)
+
+
+def test_axes_mask_order_and_reverse():
+    ax = O.coupling_axes(5, [5, 1, 2], n=1)          # Axes.jl:88-98
+    assert ax["axis_af"] == [5, 1, 2]                 # user order kept
+    assert ax["axis_id"] == [3, 4]                    # sorted complement
+    assert ax["axis_nn"] == [1, 4, 5]                 # θ first, then id .+ n
+    r = O.reverse_axes(ax)                            # Axes.jl:129-134
+    assert r["axis_id"] == [5, 1, 2] and r["axis_af"] == [3, 4]
+    assert r["axis_nn"] == [1, 6, 2, 3]               # old af order, unsorted
+    assert O.is_reverse(ax, r)
+
+
+# --- test/runtests.jl:43-64 ("real_NVP") -------------------------------------
+@pytest.mark.parametrize("mask", [None, [1, 3, 5, 7]])
+def test_rnvp_roundtrip_and_exact_ldj_cancellation(mask):
+    rng = np.random.default_rng(0)
+    ax = O.coupling_axes_cut(7, 3, n=2) if mask is None else O.coupling_axes(7, mask, n=2)
+    layer = O.rnvp_layer(rng, ax)
+    z1 = np.full((7, 10), 0.2, np.float32)
+    th = np.full((2, 10), 0.1, np.float32)
+    x, l1 = O.rnvp_forward(layer, z1, th, np.float32)
+    z2, l2 = O.rnvp_backward(layer, x.astype(np.float32), th, np.float32)
+    np.testing.assert_allclose(z2, z1, rtol=np.sqrt(np.finfo(np.float32).eps))
+    assert np.all(l1 + l2 == 0)       # `.≈ 0f0` with default tolerances ⇒ exact zero
+
+
+# --- test/runtests.jl:66-95 ("chain") ----------------------------------------
+def _runtests_chain(rng):
+    l1 = O.rnvp_layer(rng, O.coupling_axes(7, [1, 3, 5, 7], n=2))
+    l2 = O.rnvp_layer(rng, O.coupling_axes(7, [4, 2, 5, 1, 6], n=2))
+    blk = O.coupling_block(rng, O.coupling_axes(7, [4, 2, 5, 1], n=2))
+    x1 = np.full((7, 10), 0.2, np.float32)
+    x1[:, 1] = 0.4
+    th = np.full((2, 10), 0.1, np.float32)
+    th[0, 1] = 0.4
+    chain = {"kind": "chain", "layers": [l1, l2, blk, O.normalization_layer(x1)]}
+    return chain, x1, th
+
+
+def test_chain_roundtrip():
+    chain, x1, th = _runtests_chain(np.random.default_rng(1))
+    z, lb = O.backward(chain, x1, th, np.float32)
+    x2, lf = O.forward(chain, z.astype(np.float32), th, np.float32)
+    np.testing.assert_allclose(x2, x1, rtol=np.sqrt(np.finfo(np.float32).eps), atol=1e-6)
+    assert np.all(np.abs(lf + lb) <= 2e-6)
+
+
+# --- test/runtests.jl:7-31 ("data") and the datatest.jld2 fixture -----------
+def test_normalize_input_range():
+    th = np.full((2, 10), 0.1, np.float32)
+    th[0, 1] = 0.4
+    y = O.normalize_input(th, th.min(axis=1), th.max(axis=1))
+    assert y.max() <= 1 and y.min() >= 0
+    assert np.all(y[1] == 0)          # max == min row → 0 (Data.jl:216)
+
+
+def test_datatest_fixture():
+    x = np.load(os.path.join(GOLDEN, "datatest_x.npy"))
+    th = np.load(os.path.join(GOLDEN, "datatest_theta.npy"))
+    assert x.shape == (5, 1000) and x.dtype == np.float32
+    assert th.shape == (1, 1000)
+    vals, counts = np.unique(th, return_counts=True)
+    assert list(vals) == [-1.0, 2.0] and list(counts) == [500, 500]
+    nl = O.normalization_layer(x, -1.0, 1.0)
+    # backward maps the data range [x_min, x_max] onto [α, β] (Normalization.jl:64-77)
+    y, _ = O.norm_backward(nl, x, None, np.float32)
+    assert np.allclose(y.min(axis=1), -1, atol=1e-6) and np.allclose(y.max(axis=1), 1, atol=1e-6)
+
+
+def test_dflt_theta_shapes():
+    # Data.jl:47-53 doctests
+    assert O.dflt_theta((2, 3)).shape == (0, 2, 3)
+    assert O.dflt_theta((4, 5)).shape == (0, 4, 5)
+
+
+# --- doctests src/Layers.jl:99-104, src/Blocks.jl:51-59 -----------------------
+def test_doctest_parameter_counts():
+    rng = np.random.default_rng(0)
+    ax = O.coupling_axes(3, [1, 3], n=2)
+    s = O.default_net(rng, 3, 2, n_sub=1, hidden=10, act="tanh")
+    t = O.default_net(rng, 3, 2, n_sub=2, hidden=10, act="tanh")
+    assert [l["W"].shape[1] for l in s[:1]] + [l["W"].shape[0] for l in s] == [3, 10, 2]
+    assert O.num_params(s) == 62 and O.num_params(t) == 172
+    r = O.reverse_axes(ax)
+    s2 = O.default_net(rng, len(r["axis_nn"]), len(r["axis_af"]), n_sub=1, hidden=10)
+    t2 = O.default_net(rng, len(r["axis_nn"]), len(r["axis_af"]), n_sub=2, hidden=10)
+    assert O.num_params(s2) == 61 and O.num_params(t2) == 171
+
+
+# --- golden fixtures -----------------------------------------------------------
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4"])
+def test_golden_matches_oracle(name):
+    spec, g, meta = G.load(name)
+    if not meta["weights_stored"]:
+        assert G.weights_checksum(spec) == pytest.approx(meta["weights_checksum"], rel=1e-12)
+    x, lf = O.forward(spec, g["z"], g["theta"], np.float64)
+    np.testing.assert_array_equal(x, g["x_fwd"])
+    np.testing.assert_array_equal(lf, g["ldj_fwd"])
+    z, lb = O.backward(spec, g["x_in"], g["theta"], np.float64)
+    np.testing.assert_array_equal(z, g["z_bwd"])
+    np.testing.assert_array_equal(lb, g["ldj_bwd"])
+    # invertibility of the fp64 oracle itself
+    assert close(g["z_bwd"], g["z"], rtol=1e-5)[0]
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4"])
+def test_fp32_oracle_within_parity_tolerance(name):
+    """The Flux-like fp32 evaluation meets the 1e-5 criterion vs fp64 — so the
+    criterion is attainable by any correct fp32 implementation."""
+    spec, g, _ = G.load(name)
+    x32, l32 = O.forward(spec, g["z"], g["theta"], np.float32)
+    assert close(x32, g["x_fwd"])[0] and close(l32, g["ldj_fwd"])[0]
+
+
+def test_logpdf_matches_mvnormal():
+    rng = np.random.default_rng(3)
+    z = rng.standard_normal((5, 7))
+    lp = O.mvnormal_logpdf(z, np.float64)
+    ref = -0.5 * (5 * np.log(2 * np.pi) + np.sum(z * z, axis=0))
+    np.testing.assert_allclose(lp, ref, rtol=1e-14)
