@@ -55,6 +55,9 @@ constexpr double kLog2Pi = 1.8378770664093453;  // log(2π)
 
 }  // namespace
 
+struct df_chain;
+static size_t lds_for_tiles(const df_chain* c, int t);
+
 struct df_chain {
     df::Plan plan;
     int device = 0;
@@ -70,9 +73,40 @@ struct df_chain {
     double* d_partial = nullptr;
     int64_t partial_cap = 0;
     int stage_bytes = 0;
+    int n_stage_bufs = 1;
+    void* d_sched = nullptr;    // [fwd schedule | bwd schedule]
+    void* d_ulayers = nullptr;  // specialised-kernel descriptors
+    int n_cu = 0;
+    int occ[4][df::kMaxTilesPerWave + 1] = {};  // resident workgroups per CU, by mode and tiles
     int tab_bytes = 0;
     size_t lds = 0;
 };
+
+static size_t lds_for_tiles(const df_chain* c, int t) {
+    const df::Plan& P = c->plan;
+    return (size_t)c->stage_bytes * c->n_stage_bufs + c->tab_bytes +
+           (size_t)df::kWavesPerBlock * 16 * t * P.stride * 4;
+}
+
+// Tiles per wave for this launch: balance the grid over the resident
+// workgroup slots (time ~ rounds × (tiles + fixed per-round overhead)).
+static int choose_tiles(const df_chain* c, int mode, int64_t batch) {
+    const df::Plan& P = c->plan;
+    int best = 1;
+    double best_cost = 1e300;
+    for (int t = 1; t <= P.tiles; ++t) {
+        const int64_t per_block = (int64_t)df::kWavesPerBlock * 16 * t;
+        const int64_t nwg = (batch + per_block - 1) / per_block;
+        const int64_t slots = (int64_t)c->n_cu * (c->occ[mode][t] > 0 ? c->occ[mode][t] : 1);
+        const int64_t rounds = (nwg + slots - 1) / slots;
+        const double cost = (double)rounds * (t + 0.5);
+        if (cost <= best_cost) {
+            best_cost = cost;
+            best = t;
+        }
+    }
+    return best;
+}
 
 extern "C" {
 
@@ -93,7 +127,7 @@ int df_chain_destroy(df_chain* c) {
     if (!c) return DF_OK;
     DeviceGuard gd(c->device);
     void* ptrs[] = {c->d_layers, c->d_denses, c->d_chunks, c->d_stages, c->d_blob,
-                    c->d_tables, c->d_params, c->d_bounds, c->d_partial};
+                    c->d_tables, c->d_params, c->d_bounds, c->d_partial, c->d_sched, c->d_ulayers};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;
@@ -122,10 +156,13 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
         return set_err(DF_ERR_HIP, "hipSetDevice failed");
     }
     const df::Plan& P = c->plan;
+    std::vector<int32_t> sched_all(P.sched_fwd);
+    sched_all.insert(sched_all.end(), P.sched_bwd.begin(), P.sched_bwd.end());
     if ((rc = upload(P.layers, &c->d_layers)) != DF_OK || (rc = upload(P.denses, &c->d_denses)) != DF_OK ||
         (rc = upload(P.chunks, &c->d_chunks)) != DF_OK || (rc = upload(P.stages, &c->d_stages)) != DF_OK ||
         (rc = upload(P.blob, &c->d_blob)) != DF_OK || (rc = upload(P.tables, &c->d_tables)) != DF_OK ||
-        (rc = upload(P.params, &c->d_params)) != DF_OK) {
+        (rc = upload(P.params, &c->d_params)) != DF_OK || (rc = upload(sched_all, &c->d_sched)) != DF_OK ||
+        (rc = upload(P.ulayers, &c->d_ulayers)) != DF_OK) {
         std::string m = g_err;
         df_chain_destroy(c);
         return set_err(rc, m);
@@ -135,21 +172,34 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
         df_chain_destroy(c);
         return set_err(DF_ERR_NOMEM, "hipMalloc failed (θ bounds)");
     }
-    // LDS carve: [stage buffer | tables | state tile]; the stage area also hosts the
-    // fp64 workgroup reduction of the logpdf epilogue (>= 64 B).
-    c->stage_bytes = (P.stage_max + 15) / 16 * 16;
-    if (c->stage_bytes < 64) c->stage_bytes = 64;
+    // LDS carve: [stage buffer(s) | tables | state tile]; the stage area also hosts
+    // the fp64 workgroup reduction of the logpdf epilogue (>= 64 B).
+    c->stage_bytes = P.stage_max < 1024 ? 1024 : P.stage_max;
+    c->n_stage_bufs = P.stages.size() > 1 ? 2 : 1;
     c->tab_bytes = ((int)P.tables.size() * 4 + 15) / 16 * 16;
-    c->lds = (size_t)c->stage_bytes + c->tab_bytes + (size_t)P.samples_per_block * P.stride * 4;
+    c->lds = (size_t)c->stage_bytes * c->n_stage_bufs + c->tab_bytes +
+             (size_t)P.samples_per_block * P.stride * 4;
     if (c->lds > 160 * 1024) {
         df_chain_destroy(c);
         return set_err(DF_ERR_UNSUPPORTED, "chain needs more than 160 KiB of LDS per workgroup");
     }
-    e = df::set_kernel_lds_limit(P.ht, c->lds);
+    e = df::set_kernel_lds_limit(P.ht, P.uniform != 0, c->lds);
     if (e != hipSuccess) {
         df_chain_destroy(c);
         return hip_err(e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
     }
+    // occupancy by mode and tiles per wave (for the per-launch tile choice)
+    if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->n_cu < 1)
+        c->n_cu = 256;
+    for (int mode = 0; mode < 4; ++mode)
+        for (int t = 1; t <= P.tiles; ++t) {
+            int blocks = 1;
+            if (df::kernel_occupancy(P.ht, mode, P.outv != 0, P.uniform != 0, lds_for_tiles(c, t), &blocks) !=
+                    hipSuccess ||
+                blocks < 1)
+                blocks = 1;
+            c->occ[mode][t] = blocks;
+        }
     *out = c;
     return DF_OK;
 }
@@ -224,7 +274,8 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
 
     DeviceGuard gd(c->device);
     if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
-    const int64_t S = P.samples_per_block;
+    const int tiles = choose_tiles(c, mode, batch);
+    const int64_t S = (int64_t)df::kWavesPerBlock * 16 * tiles;
     const int64_t grid = (batch + S - 1) / S;
     if (grid > 0x7fffffff) return set_err(DF_ERR_UNSUPPORTED, "batch too large for one launch");
     if (sum_out && grid > c->partial_cap) {
@@ -256,15 +307,23 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     a.d = P.d;
     a.n = P.n;
     a.stride = P.stride;
+    a.tiles = tiles;
+    a.ulayers = static_cast<const df::ULayer*>(c->d_ulayers);
     a.n_layers = P.n_layers;
     a.tab_ints = (int)P.tables.size();
     a.tab_bytes = c->tab_bytes;
     a.stage_bytes = c->stage_bytes;
+    a.n_stage_bufs = c->n_stage_bufs;
+    a.sched_fwd = static_cast<const int32_t*>(c->d_sched);
+    a.sched_bwd = a.sched_fwd + P.sched_fwd.size();
+    a.n_sched_fwd = (int)P.sched_fwd.size();
+    a.n_sched_bwd = (int)P.sched_bwd.size();
     // Distributions.mvnormal_c0: -(d * log2π + logdetcov)/2 in Float32, logdet(I) = 0
     a.c0 = -((float)P.d * (float)kLog2Pi + 0.f) / 2.f;
 
     hipStream_t st = static_cast<hipStream_t>(stream);
-    hipError_t e = df::launch_chain(P.ht, mode, P.outv != 0, a, (unsigned)grid, c->lds, st);
+    hipError_t e = df::launch_chain(P.ht, mode, P.outv != 0, P.uniform != 0, a, (unsigned)grid,
+                                    lds_for_tiles(c, tiles), st);
     if (e != hipSuccess) return hip_err(e, "chain kernel launch");
     if (sum_out) {
         e = df::launch_reduce_partials(c->d_partial, grid, sum_out, st);

@@ -24,7 +24,15 @@ hipError_t launch_reduce_partials(const double* part, int64_t n, double* out, hi
     return hipGetLastError();
 }
 
-hipError_t set_kernel_lds_limit(int ht, size_t lds) {
+hipError_t set_kernel_lds_limit(int ht, bool uniform, size_t lds) {
+    if (uniform) {
+        switch (ht) {
+            case 1: return set_uniform_lds_limit_ht<1>(lds);
+            case 2: return set_uniform_lds_limit_ht<2>(lds);
+            case 4: return set_uniform_lds_limit_ht<4>(lds);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (ht) {
         case 1: return set_lds_limit_ht<1>(lds);
         case 2: return set_lds_limit_ht<2>(lds);
@@ -35,8 +43,35 @@ hipError_t set_kernel_lds_limit(int ht, size_t lds) {
     }
 }
 
-hipError_t launch_chain(int ht, int mode, bool outv, const ChainArgs& a, unsigned grid, size_t lds,
+hipError_t kernel_occupancy(int ht, int mode, bool outv, bool uniform, size_t lds, int* blocks) {
+    if (uniform) {
+        switch (ht) {
+            case 1: return uniform_occupancy_ht<1>(mode, outv, lds, blocks);
+            case 2: return uniform_occupancy_ht<2>(mode, outv, lds, blocks);
+            case 4: return uniform_occupancy_ht<4>(mode, outv, lds, blocks);
+            default: return hipErrorInvalidValue;
+        }
+    }
+    switch (ht) {
+        case 1: return chain_occupancy_ht<1>(mode, outv, lds, blocks);
+        case 2: return chain_occupancy_ht<2>(mode, outv, lds, blocks);
+        case 4: return chain_occupancy_ht<4>(mode, outv, lds, blocks);
+        case 8: return chain_occupancy_ht<8>(mode, outv, lds, blocks);
+        case 16: return chain_occupancy_ht<16>(mode, outv, lds, blocks);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_chain(int ht, int mode, bool outv, bool uniform, const ChainArgs& a, unsigned grid, size_t lds,
                         hipStream_t st) {
+    if (uniform) {
+        switch (ht) {
+            case 1: return launch_uniform_ht<1>(mode, outv, a, grid, lds, st);
+            case 2: return launch_uniform_ht<2>(mode, outv, a, grid, lds, st);
+            case 4: return launch_uniform_ht<4>(mode, outv, a, grid, lds, st);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (ht) {
         case 1: return launch_chain_ht<1>(mode, outv, a, grid, lds, st);
         case 2: return launch_chain_ht<2>(mode, outv, a, grid, lds, st);

@@ -14,13 +14,6 @@ enum : int {
     MODE_LOGPDF = 3        // backward + MvNormal(0, I) logpdf + ldj
 };
 
-// 16-sample MFMA column tiles per wave for a kernel variant (must match the
-// planner: Plan::tiles).
-#ifndef DF_TILES_SMALL
-#define DF_TILES_SMALL 1
-#endif
-constexpr int tiles_per_wave(int ht) { return ht <= 4 ? DF_TILES_SMALL : 1; }
-
 struct ChainArgs {
     const float* zin;
     const float* theta;
@@ -30,6 +23,7 @@ struct ChainArgs {
     double* partial;
     int64_t batch;
     const DevLayer* layers;
+    const ULayer* ulayers;   // specialised kernel only
     const DevDense* denses;
     const DevChunk* chunks;
     const DevStage* stages;
@@ -39,9 +33,15 @@ struct ChainArgs {
     const float* tmin;   // θ bounds; nullptr → θ used as given
     const float* tmax;
     int d, n, stride, n_layers;
+    int tiles;           // 16-sample tiles per wave resident in LDS (Plan::tiles)
     int tab_ints;
     int tab_bytes;       // LDS bytes reserved for tables (16-B multiple)
-    int stage_bytes;     // LDS bytes reserved for the stage buffer (16-B multiple)
+    int stage_bytes;     // LDS bytes of ONE stage buffer (multiple of 1 KiB)
+    int n_stage_bufs;    // 1 (single-stage chain) or 2 (double-buffered)
+    const int32_t* sched_fwd;
+    const int32_t* sched_bwd;
+    int n_sched_fwd;
+    int n_sched_bwd;
     float c0;            // -(d·log2π)/2
 };
 
@@ -50,11 +50,20 @@ template <int HT>
 hipError_t launch_chain_ht(int mode, bool outv, const ChainArgs& a, unsigned grid, size_t lds, hipStream_t st);
 template <int HT>
 hipError_t set_lds_limit_ht(size_t lds);
+template <int HT>
+hipError_t launch_uniform_ht(int mode, bool outv, const ChainArgs& a, unsigned grid, size_t lds, hipStream_t st);
+template <int HT>
+hipError_t set_uniform_lds_limit_ht(size_t lds);
+template <int HT>
+hipError_t uniform_occupancy_ht(int mode, bool outv, size_t lds, int* blocks);
+template <int HT>
+hipError_t chain_occupancy_ht(int mode, bool outv, size_t lds, int* blocks);
 
 // Dispatch over the variant (df_common.hip).
-hipError_t set_kernel_lds_limit(int ht, size_t lds);
-hipError_t launch_chain(int ht, int mode, bool outv, const ChainArgs& a, unsigned grid, size_t lds,
-                        hipStream_t st);
+hipError_t set_kernel_lds_limit(int ht, bool uniform, size_t lds);
+hipError_t launch_chain(int ht, int mode, bool outv, bool uniform, const ChainArgs& a, unsigned grid,
+                        size_t lds, hipStream_t st);
+hipError_t kernel_occupancy(int ht, int mode, bool outv, bool uniform, size_t lds, int* blocks);
 hipError_t launch_reduce_partials(const double* part, int64_t n, double* out, hipStream_t st);
 
 }  // namespace df

@@ -44,9 +44,10 @@ struct Item {
 
 class Packer {
 public:
-    explicit Packer(Plan& p) : P(p) {}
+    Packer(Plan& p, int cap) : P(p), cap_(cap) {}
 
-    int remaining() const { return cur_ < 0 ? 0 : kStageCap - used_; }
+    int remaining() const { return cur_ < 0 ? 0 : cap_ - used_; }
+    int cap() const { return cap_; }
 
     void begin_stage() {
         close();
@@ -60,8 +61,8 @@ public:
     // Reserve `bytes` (multiple of 16) in the current stage (opening one if
     // needed).  Returns {stage, byte offset in stage}.
     std::pair<int, int> alloc(int bytes) {
-        if (bytes > kStageCap) fail(DF_ERR_UNSUPPORTED, "packed item exceeds the LDS stage buffer");
-        if (cur_ < 0 || used_ + bytes > kStageCap) begin_stage();
+        if (bytes > cap_) fail(DF_ERR_UNSUPPORTED, "packed item exceeds the LDS stage buffer");
+        if (cur_ < 0 || used_ + bytes > cap_) begin_stage();
         int off = used_;
         used_ += bytes;
         P.blob.resize((size_t)P.stages[cur_].src_off + used_, 0);
@@ -72,8 +73,11 @@ public:
         return reinterpret_cast<float*>(P.blob.data() + P.stages[stage].src_off + off);
     }
 
+    // Pad the open stage to the DMA granularity and record its size.
     void close() {
         if (cur_ >= 0) {
+            used_ = round_up(used_, kStageAlign);
+            P.blob.resize((size_t)P.stages[cur_].src_off + used_, 0);
             P.stages[cur_].bytes = used_;
             P.stage_max = std::max(P.stage_max, used_);
         }
@@ -81,6 +85,7 @@ public:
 
 private:
     Plan& P;
+    int cap_;
     int cur_ = -1;
     int used_ = 0;
 };
@@ -114,7 +119,8 @@ void check_net(const df_dense_desc* net, int nd, int in_dim, int out_dim, const 
 
 size_t plan_lds_bytes(const Plan& p) {
     size_t tab = (size_t)round_up((int)p.tables.size() * 4, 16);
-    return (size_t)p.stage_max + tab + (size_t)p.samples_per_block * p.stride * 4;
+    const int nbuf = p.stages.size() > 1 ? 2 : 1;
+    return (size_t)nbuf * p.stage_max + tab + (size_t)p.samples_per_block * p.stride * 4;
 }
 
 int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
@@ -131,7 +137,7 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
         P.d = d;
         P.n = n;
         P.n_layers = desc->n_layers;
-        P.stride = n + d + 1;                 // [θ | z | 0]
+        P.stride = n + d + 3;                 // [θ | z | 0 | ldj_chain | ldj_elem]
         if (P.stride % 2 == 0) P.stride += 1; // odd stride: spread LDS banks
 
         // ---------- pass 0: output path of the conditioner nets ----------
@@ -193,11 +199,35 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
         }
         P.ht = pow2_tiles(max_tiles);
         if (P.ht > kMaxHidden / 16) fail(DF_ERR_UNSUPPORTED, "hidden width > 256");
-        P.tiles = P.ht <= 4 ? kTilesSmall : 1;
-        P.samples_per_block = kWavesPerBlock * 16 * P.tiles;
 
         // ---------- pass 2: packing ----------
-        Packer pk(P);
+        // Whole chain in one stage when it is small (loaded once per workgroup);
+        // otherwise 24 KiB stages, double-buffered in LDS, one net per stage
+        // whenever a net fits.
+        int64_t total_bytes = 0;
+        for (int li = 0; li < desc->n_layers; ++li) {
+            const df_layer_desc& L = desc->layers[li];
+            if (L.kind == DF_LAYER_NORM) continue;
+            auto net_bytes = [&](const df_dense_desc* net, int nd) {
+                int64_t b = 0;
+                int prev_tiles = 0;
+                for (int k = 0; k < nd; ++k) {
+                    const bool last = (k + 1 == nd);
+                    if (last && all_valu) {
+                        b += round_up((net[k].out_dim * 16 * prev_tiles + 4) * 4, 16);
+                    } else {
+                        const int mt = (net[k].out_dim + 15) / 16;
+                        const int ks = (k == 0) ? (L.n_nn + 3) / 4 : 4 * prev_tiles;
+                        b += (int64_t)((ks + 3) / 4) * mt * 1024 + mt * 64;
+                        prev_tiles = mt;
+                    }
+                }
+                return b;
+            };
+            if (L.kind == DF_LAYER_RNVP) total_bytes += net_bytes(L.s_net, L.n_dense_s);
+            total_bytes += net_bytes(L.t_net, L.n_dense_t);
+        }
+        Packer pk(P, total_bytes <= kSingleStageCap ? kSingleStageCap : kStageCap);
         const int zero_slot = n + d;
         for (int li = 0; li < desc->n_layers; ++li) {
             const df_layer_desc& L = desc->layers[li];
@@ -276,10 +306,19 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
             else { DL.s_dense0 = 0; DL.s_ndense = 0; }
             add_net(L.t_net, L.n_dense_t, &DL.t_dense0, &DL.t_ndense);
 
-            // Keep a layer inside one stage whenever it fits.
+            // Keep a layer — else each net — inside one stage whenever it fits.
             int layer_bytes = 0;
             for (auto& it : items) layer_bytes += it.bytes;
-            if (layer_bytes > pk.remaining()) pk.begin_stage();
+            if (layer_bytes > pk.remaining() && layer_bytes <= pk.cap()) pk.begin_stage();
+            const int t_first_dense = DL.t_dense0;
+            auto net_bytes_from = [&](size_t i0) {
+                int b = 0;
+                for (size_t i = i0; i < items.size(); ++i) {
+                    if ((items[i].dense >= t_first_dense) != (items[i0].dense >= t_first_dense)) break;
+                    b += items[i].bytes;
+                }
+                return b;
+            };
 
             // dense index → source Dense for packing
             auto src_of = [&](int dense_idx) -> const df_dense_desc& {
@@ -288,7 +327,13 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                 return L.t_net[dense_idx - DL.t_dense0];
             };
 
-            for (auto& it : items) {
+            for (size_t ii = 0; ii < items.size(); ++ii) {
+                const Item& it = items[ii];
+                const bool net_start = (ii == 0) || ((items[ii - 1].dense >= t_first_dense) != (it.dense >= t_first_dense));
+                if (net_start && ii > 0) {
+                    const int nb = net_bytes_from(ii);
+                    if (nb > pk.remaining() && nb <= pk.cap()) pk.begin_stage();
+                }
                 DevDense& DD = P.denses[it.dense];
                 const df_dense_desc& D = src_of(it.dense);
                 const int out = D.out_dim, in = D.in_dim;
@@ -353,6 +398,144 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
             count(L.t_net, L.n_dense_t);
         }
         pk.close();
+
+        // Stage schedules: the order in which the kernel's ensure_stage() calls
+        // ask for stages (forward: s-net then t-net per layer; inverse: layers
+        // reversed, t-net then s-net), consecutive duplicates removed.
+        auto sched = [&](bool fwd) {
+            std::vector<int32_t> out;
+            auto push = [&](int s) {
+                if (out.empty() || out.back() != s) out.push_back(s);
+            };
+            auto net = [&](int d0, int nd) {
+                for (int k = 0; k < nd; ++k) {
+                    const DevDense& D = P.denses[d0 + k];
+                    if (D.out_valu) {
+                        push(D.w3_stage);
+                    } else {
+                        for (int c = 0; c < D.n_chunks; ++c) push(P.chunks[D.chunk0 + c].stage);
+                        push(D.bias_stage);
+                    }
+                }
+            };
+            for (int it = 0; it < P.n_layers; ++it) {
+                const DevLayer& L = P.layers[fwd ? it : P.n_layers - 1 - it];
+                if (L.kind == DF_LAYER_NORM) continue;
+                if (fwd) {
+                    net(L.s_dense0, L.s_ndense);
+                    net(L.t_dense0, L.t_ndense);
+                } else {
+                    net(L.t_dense0, L.t_ndense);
+                    net(L.s_dense0, L.s_ndense);
+                }
+            }
+            return out;
+        };
+        P.sched_fwd = sched(true);
+        P.sched_bwd = sched(false);
+
+        // Tiles of 16 samples per wave kept resident in LDS.  When every net lives
+        // in one stage, a stage switch serves all of a wave's tiles, so take as
+        // many as fit two workgroups per CU (<= 80 KiB each); otherwise one tile.
+        bool resident = true;
+        for (const DevLayer& L : P.layers) {
+            if (L.kind == DF_LAYER_NORM) continue;
+            auto one_stage = [&](int d0, int nd) {
+                int st = -1;
+                for (int k = 0; k < nd; ++k) {
+                    const DevDense& D = P.denses[d0 + k];
+                    std::vector<int> ss;
+                    if (D.out_valu) ss.push_back(D.w3_stage);
+                    else {
+                        for (int c = 0; c < D.n_chunks; ++c) ss.push_back(P.chunks[D.chunk0 + c].stage);
+                        ss.push_back(D.bias_stage);
+                    }
+                    for (int x : ss) {
+                        if (st < 0) st = x;
+                        if (x != st) return false;
+                    }
+                }
+                return true;
+            };
+            resident = resident && one_stage(L.s_dense0, L.s_ndense) && one_stage(L.t_dense0, L.t_ndense);
+        }
+        // Specialised-kernel descriptors when every net has the default shape.
+        P.uniform = (resident && P.ht <= 4) ? 1 : 0;
+        auto make_unet = [&](int d0, int nd, UNet* u) -> bool {
+            if (nd < 2) return false;
+            const DevDense& D0 = P.denses[d0];
+            if (D0.in_kind != IN_STATE || D0.ks > 4 || D0.mt != P.ht || D0.n_chunks != 1) return false;
+            const DevChunk& C0 = P.chunks[D0.chunk0];
+            u->stage = C0.stage;
+            u->ks = D0.ks;
+            u->nh = nd - 2;
+            u->off_w0 = C0.lds_off;
+            u->off_b0 = D0.bias_lds;
+            u->act0 = D0.act;
+            u->acth = DF_ACT_IDENTITY;
+            u->hstride = P.ht * P.ht * 1024 + 64 * P.ht;
+            for (int k = 1; k + 1 < nd; ++k) {
+                const DevDense& D = P.denses[d0 + k];
+                if (D.mt != P.ht || D.kt_in != P.ht || D.n_chunks != 1) return false;
+                const DevChunk& C = P.chunks[D.chunk0];
+                if (C.kq_begin != 0 || C.kq_end != P.ht) return false;
+                if (k == 1) {
+                    u->off_h = C.lds_off;
+                    u->acth = D.act;
+                }
+                if (D.act != u->acth) return false;
+                if (C.lds_off != u->off_h + (k - 1) * u->hstride) return false;
+                if (D.bias_lds != C.lds_off + P.ht * P.ht * 1024) return false;
+            }
+            if (nd == 2) u->off_h = 0;
+            const DevDense& DL = P.denses[d0 + nd - 1];
+            if (DL.kt_in != P.ht) return false;
+            u->n_out = DL.n_out;
+            u->act_out = DL.act;
+            if (DL.out_valu) {
+                u->off_out = DL.w3_lds;
+            } else {
+                if (DL.n_chunks != 1) return false;
+                const DevChunk& C = P.chunks[DL.chunk0];
+                if (C.kq_begin != 0 || C.kq_end != P.ht) return false;
+                u->off_out = C.lds_off;
+                if (DL.bias_lds != C.lds_off + P.ht * DL.mt * 1024) return false;
+            }
+            return true;
+        };
+        if (P.uniform) {
+            for (const DevLayer& L : P.layers) {
+                ULayer U{};
+                U.kind = L.kind;
+                U.elem_start = L.elem_start;
+                U.elem_end = L.elem_end;
+                U.n_af = L.n_af;
+                U.feat_tab = L.feat_tab;
+                U.af_tab = L.af_tab;
+                U.norm_off = L.norm_off;
+                U.alpha = L.alpha;
+                U.beta = L.beta;
+                U.ldj_const = L.ldj_const;
+                if (L.kind != DF_LAYER_NORM) {
+                    bool ok = make_unet(L.t_dense0, L.t_ndense, &U.t);
+                    if (L.kind == DF_LAYER_RNVP) ok = ok && make_unet(L.s_dense0, L.s_ndense, &U.s);
+                    if (!ok) {
+                        P.uniform = 0;
+                        break;
+                    }
+                }
+                P.ulayers.push_back(U);
+            }
+            if (!P.uniform) P.ulayers.clear();
+        }
+
+        const int nbuf = P.stages.size() > 1 ? 2 : 1;
+        const int fixed = nbuf * P.stage_max + round_up((int)P.tables.size() * 4, 16);
+        const int per_tile = kWavesPerBlock * 16 * P.stride * 4;
+        P.tiles = 1;
+        if (resident)
+            while (P.tiles < kMaxTilesPerWave && fixed + (P.tiles + 1) * per_tile <= kLdsPerBlockTarget) ++P.tiles;
+        P.samples_per_block = kWavesPerBlock * 16 * P.tiles;
         if ((int)P.tables.size() > kMaxTableInts) fail(DF_ERR_UNSUPPORTED, "chain index tables exceed 16 KiB");
         if (P.stages.empty()) {  // normalization-only chain: keep one empty stage record
             P.stage_max = 0;

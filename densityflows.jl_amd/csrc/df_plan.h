@@ -26,12 +26,12 @@ constexpr int kMaxState = 64;        // n + d (conditioner input <= 64 features)
 constexpr int kMaxHidden = 256;      // widest Dense (16 MFMA row tiles)
 constexpr int kMaxAf = 32;           // transformed dims per coupling layer
 constexpr int kMaxLayers = 4096;
-constexpr int kStageCap = 48 * 1024; // bytes of the LDS weight stage buffer
+constexpr int kStageCap = 24 * 1024;       // LDS weight stage buffer (double-buffered)
+constexpr int kSingleStageCap = 64 * 1024; // a whole chain this small lives in one stage
+constexpr int kStageAlign = 1024;          // one global->LDS DMA wave instruction (64 lanes x 16 B)
 constexpr int kMaxTableInts = 4096;  // 16 KiB of int32 tables in LDS
-#ifndef DF_TILES_SMALL
-#define DF_TILES_SMALL 1
-#endif
-constexpr int kTilesSmall = DF_TILES_SMALL;  // sample tiles per wave for hidden <= 64
+constexpr int kMaxTilesPerWave = 8;          // 16-sample tiles per wave resident in LDS
+constexpr int kLdsPerBlockTarget = 80 * 1024; // two workgroups per CU
 
 enum : int32_t { IN_STATE = 0, IN_HIDDEN = 1 };
 
@@ -70,6 +70,27 @@ struct DevLayer {
     float alpha, beta, ldj_const, pad;
 };
 
+// Compact descriptors of the specialised kernel (df_uniform_impl.h): every
+// conditioner is Dense(in<=16, H) → nh × Dense(H, H) → Dense(H, out) with
+// H = 16·HT, laid out contiguously in ONE stage.
+struct UNet {
+    int32_t stage;
+    int32_t ks;        // first-Dense k-steps (<= 4)
+    int32_t nh;        // hidden H×H Denses
+    int32_t n_out;
+    int32_t off_w0, off_b0;   // byte offsets in the stage
+    int32_t off_h, hstride;   // hidden k: W at off_h + k*hstride, bias right after W
+    int32_t off_out;          // VALU: W[n_out][H] then b[4]; MFMA: frags then bias
+    int32_t act0, acth, act_out;
+};
+
+struct ULayer {
+    int32_t kind, elem_start, elem_end, n_af;
+    int32_t feat_tab, af_tab, norm_off, pad0;
+    float alpha, beta, ldj_const, pad1;
+    UNet s, t;
+};
+
 struct DevStage {
     int64_t src_off;     // byte offset in the blob
     int32_t bytes;       // multiple of 16
@@ -80,10 +101,14 @@ struct Plan {
     int d = 0, n = 0, n_layers = 0;
     int stride = 0;          // floats per sample row of the LDS state tile
     int ht = 0;              // kernel variant: max row tiles (1,2,4,8,16)
-    int tiles = 0;           // 16-sample MFMA column tiles per wave
+    int tiles = 0;           // 16-sample tiles per wave resident in LDS
     int outv = 0;            // kernel variant: final Dense as VALU GEMV (<= 4 outputs)
+    int uniform = 0;         // every layer fits the specialised kernel (ulayers valid)
+    std::vector<ULayer> ulayers;
     int samples_per_block = 0;
-    int stage_max = 0;       // largest stage (bytes)
+    int stage_max = 0;       // largest stage (bytes, multiple of kStageAlign)
+    std::vector<int32_t> sched_fwd;  // stage ids in the order a forward pass needs them
+    std::vector<int32_t> sched_bwd;  // ... and a backward (inverse) pass
     std::vector<DevLayer> layers;
     std::vector<DevDense> denses;
     std::vector<DevChunk> chunks;
@@ -99,7 +124,7 @@ struct Plan {
 // reference's exception text where one exists.
 int build_plan(const df_chain_desc* desc, Plan* out, std::string* err);
 
-// Workgroup LDS bytes for a plan (stage buffer + tables + state tile).
+// Workgroup LDS bytes for a plan (stage buffers + tables + state tile).
 size_t plan_lds_bytes(const Plan& p);
 
 }  // namespace df
