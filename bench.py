@@ -36,24 +36,57 @@ PEAK_F32_TFLOPS = 157.3   # MI355X f32 MFMA dense peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
-def build_chain(seed=2):
-    """Config 2: FlowChain(CouplingBlock, 4, 5; hidden_dim_s=64, hidden_dim_t=64).
-    Random init: Flux glorot_uniform weights; biases U(-0.1, 0.1); the final
-    Dense of each conditioner scaled by 0.1 so the 8-layer flow stays finite."""
-    import densityflows_amd as dfa
+CONFIGS = {
+    # name: (d, n, description)
+    "cfg2": (5, 0, "config2: d=5, n=0, FlowChain(CouplingBlock, 4, 5; hidden 64) = 8 RealNVP layers, fp32"),
+    "cfg1": (5, 1, "config1: d=5, n=1, README chain: 3 RNVP layers (masks [1,2,3],[3,4,5],[5,1,2], hidden 16) "
+                   "+ NormalizationLayer(x, -1, 1), fp32"),
+    "cfg4": (32, 8, "config4: d=32, n=8, FlowChain(CouplingBlock, 8, 32; n=8, hidden 256) = 16 RealNVP layers, fp32"),
+}
 
-    rng = np.random.default_rng(seed)
-    chain = dfa.FlowChain.repeat(dfa.CouplingBlock, 4, 5, hidden_dim_s=64, hidden_dim_t=64, rng=rng)
-    for blk in chain:
-        for layer in (blk.layer_1, blk.layer_2):
-            for net in (layer.s_net, layer.t_net):
+
+def _init_nets(chain, rng):
+    """Biases U(-0.1, 0.1); final Dense of each conditioner scaled by 0.1 so the
+    deep random-init flows stay finite."""
+    from densityflows_amd.layers import RNVPCouplingLayer, NICECouplingLayer, CouplingBlock
+
+    def layers(e):
+        if isinstance(e, CouplingBlock):
+            return [e.layer_1, e.layer_2]
+        if isinstance(e, (RNVPCouplingLayer, NICECouplingLayer)):
+            return [e]
+        return []
+
+    for e in chain:
+        for layer in layers(e):
+            nets = [layer.t_net] + ([layer.s_net] if isinstance(layer, RNVPCouplingLayer) else [])
+            for net in nets:
                 for D in net:
                     D.b = ((rng.random(D.out_dim) * 2 - 1) * 0.1).astype(np.float32)
                 net[-1].W = (net[-1].W * np.float32(0.1)).astype(np.float32)
     return chain
 
 
-def cpu_baseline(chain, seconds=12.0, sample=65536):
+def build_chain(config="cfg2", seed=2):
+    """Random-init model of a BASELINE config (Flux glorot_uniform weights)."""
+    import densityflows_amd as dfa
+
+    rng = np.random.default_rng(seed)
+    if config == "cfg2":
+        chain = dfa.FlowChain.repeat(dfa.CouplingBlock, 4, 5, hidden_dim_s=64, hidden_dim_t=64, rng=rng)
+    elif config == "cfg4":
+        chain = dfa.FlowChain.repeat(dfa.CouplingBlock, 8, 32, n=8, hidden_dim_s=256, hidden_dim_t=256, rng=rng)
+    elif config == "cfg1":
+        x = np.load(os.path.join(ROOT, "tests", "golden", "datatest_x.npy"))
+        layers = [dfa.CouplingLayer(5, m, n=1, hidden_dim_s=16, hidden_dim_t=16, rng=rng)
+                  for m in ([1, 2, 3], [3, 4, 5], [5, 1, 2])]
+        chain = dfa.FlowChain(*layers, dfa.NormalizationLayer.from_data(x, -1.0, 1.0))
+    else:
+        raise SystemExit(f"unknown config {config}")
+    return _init_nets(chain, rng)
+
+
+def cpu_baseline(chain, d, n, seconds=12.0, sample=65536):
     """Oracle fp32 (Flux-like) forward+logdetJ on host cores, bounded sample."""
     from oracle import flow_oracle as O
 
@@ -66,8 +99,8 @@ def cpu_baseline(chain, seconds=12.0, sample=65536):
         threads = 1
     spec = chain.to_spec()
     rng = np.random.default_rng(0)
-    z = rng.standard_normal((5, sample)).astype(np.float32)
-    th = np.zeros((0, sample), np.float32)
+    z = rng.standard_normal((d, sample)).astype(np.float32)
+    th = rng.random((n, sample)).astype(np.float32)
     O.forward(spec, z[:, :1024], th[:, :1024], np.float32)  # warm-up
     done, t0 = 0, time.perf_counter()
     while True:
@@ -77,7 +110,7 @@ def cpu_baseline(chain, seconds=12.0, sample=65536):
         if el >= seconds:
             break
     return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": int(threads), "kind": "port",
-            "sample": f"{done} samples ({done // sample} passes of a {sample}-sample batch, config 2, "
+            "sample": f"{done} samples ({done // sample} passes of a {sample}-sample batch, "
                       f"numpy fp32 oracle with OpenBLAS sgemm) in {el:.1f} s"}
 
 
@@ -88,6 +121,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1 << 20, help="samples per GPU")
     ap.add_argument("--mode", choices=["forward", "nll"], default="forward")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg2",
+                    help="cfg2 is the headline (BASELINE configs[1]); cfg1/cfg4 are secondary measurements")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -110,26 +145,28 @@ def main():
     import densityflows_amd as dfa
     from densityflows_amd.hip import HIPChain
 
-    chain = build_chain()
-    hc = chain.hip(device=local)
+    d, n, workload = CONFIGS[args.config]
+    chain = build_chain(args.config)
+    hc = chain.hip(device=local, n_hint=n)
     info = hc.info
     B = args.batch
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
-    zbuf = torch.randn(B * 5, device=dev, generator=gen)      # Julia (5, B) column-major
+    zbuf = torch.randn(B * d, device=dev, generator=gen)      # Julia (d, B) column-major
+    thbuf = torch.rand(B * n, device=dev, generator=gen) if n > 0 else None
     xbuf = torch.empty_like(zbuf)
     ldj = torch.empty(B, device=dev)
     s64 = torch.zeros(2, dtype=torch.float64, device=dev)
 
     if args.mode == "forward":
         def step():
-            hc.run("forward", zbuf, None, xbuf, ldj, B)
+            hc.run("forward", zbuf, thbuf, xbuf, ldj, B)
     else:
-        flow = dfa.Flow(chain, metadata=dfa.MetaData("", 5, 0, np.zeros(0, np.float32), np.zeros(0, np.float32)))
+        flow = dfa.Flow(chain, metadata=dfa.MetaData("", d, n, np.zeros(n, np.float32), np.ones(n, np.float32)))
         fh = flow.hip(device=local)
-        hc.run("forward", zbuf, None, xbuf, ldj, B)  # data points x = forward(z)
+        hc.run("forward", zbuf, thbuf, xbuf, ldj, B)  # data points x = forward(z)
 
         def step():
-            fh.run_logpdf_sum(xbuf, None, s64[:1], B)
+            fh.run_logpdf_sum(xbuf, thbuf, s64[:1], B)
             s64[1] = float(B)
             if dist is not None:
                 dist.all_reduce(s64)
@@ -162,7 +199,7 @@ def main():
     kernel_s = gpu_ms / 1e3 / args.steps            # mean launch time (one launch per step)
     flop = info.flops_per_sample * B
     achieved_tflops = flop / kernel_s / 1e12
-    hbm_algo = 44.0 * B                              # read z (20 B) + write x (20 B) + ldj (4 B)
+    hbm_algo = (8.0 * d + 4.0 * n + 4.0) * B          # read z (+θ), write x, ldj
 
     if rank == 0:
         out = {
@@ -178,8 +215,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: z ~ N(0,1) generated on device; random-init weights (glorot, see bench.build_chain)",
-            "config": {"workload": "config2: d=5, n=0, FlowChain(CouplingBlock, 4, 5; hidden 64) = 8 RealNVP "
-                                   "layers, fp32" + ("" if world == 1 else f"; config3 sharding {world}x"),
+            "config": {"workload": workload + ("" if world == 1 else f"; config3 sharding {world}x"),
                        "per_gpu_batch": B, "global_batch": B * world,
                        "parallelism": f"dp{world} (independent sample shards, no data-path collective)"
                        if args.mode == "forward" else f"dp{world} + RCCL all-reduce of the NLL partial"},
@@ -190,8 +226,10 @@ def main():
                          "algorithmic_flop_per_sample": info.flops_per_sample,
                          "hbm_algorithmic_GBps": round(hbm_algo / kernel_s / 1e9, 2)},
         }
+        if args.config != "cfg2":
+            out["metric"] = out["metric"].replace("d=5 8-layer RealNVP", CONFIGS[args.config][2].split(":")[0])
         if world == 1 and not args.no_cpu and args.mode == "forward":
-            out["cpu_baseline"] = cpu_baseline(chain, seconds=args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(chain, d, n, seconds=args.cpu_seconds)
             out["vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -149,6 +150,11 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
         delete c;
         return set_err(rc, err);
     }
+    if (const char* f = std::getenv("DF_FORCE_GENERIC"))  // A/B switch for testing the generic kernel
+        if (f[0] == '1') {
+            c->plan.uniform = 0;
+            c->plan.ulayers.clear();
+        }
     c->device = device;
     DeviceGuard gd(device);
     if (!gd.ok) {
