@@ -93,9 +93,10 @@ static size_t lds_for_tiles(const df_chain* c, int t) {
 // workgroup slots (time ~ rounds × (tiles + fixed per-round overhead)).
 static int choose_tiles(const df_chain* c, int mode, int64_t batch) {
     const df::Plan& P = c->plan;
-    int best = 1;
+    int best = P.uniform ? df::kUniformTileGroup : 1;
     double best_cost = 1e300;
-    for (int t = 1; t <= P.tiles; ++t) {
+    const int step = P.uniform ? df::kUniformTileGroup : 1;
+    for (int t = step; t <= P.tiles; t += step) {
         const int64_t per_block = (int64_t)df::kWavesPerBlock * 16 * t;
         const int64_t nwg = (batch + per_block - 1) / per_block;
         const int64_t slots = (int64_t)c->n_cu * (c->occ[mode][t] > 0 ? c->occ[mode][t] : 1);

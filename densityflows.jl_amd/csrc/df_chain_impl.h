@@ -120,6 +120,9 @@ __device__ __forceinline__ void stager_start(Stager& sg, const ChainArgs& a) {
 // Make stage `s` resident (uniform across the workgroup).
 __device__ __forceinline__ void ensure_stage(int s, Stager& sg, const ChainArgs& a) {
     if (s == sg.cur) return;
+#ifdef DF_EXP_NOSYNC  // diagnostic build only: no stage switches (results are wrong)
+    if (sg.cur >= 0) { sg.cur = s; return; }
+#endif
     const int nidx = sg.idx + 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for sched[nidx] landed
     __syncthreads();                                     // ... every wave's, and buffer (nidx+1)&1 is free

@@ -535,6 +535,14 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
         P.tiles = 1;
         if (resident)
             while (P.tiles < kMaxTilesPerWave && fixed + (P.tiles + 1) * per_tile <= kLdsPerBlockTarget) ++P.tiles;
+        if (P.uniform) {  // the specialised kernel evaluates tiles in groups
+            if (P.tiles < kUniformTileGroup) {
+                P.uniform = 0;
+                P.ulayers.clear();
+            } else {
+                P.tiles -= P.tiles % kUniformTileGroup;
+            }
+        }
         P.samples_per_block = kWavesPerBlock * 16 * P.tiles;
         if ((int)P.tables.size() > kMaxTableInts) fail(DF_ERR_UNSUPPORTED, "chain index tables exceed 16 KiB");
         if (P.stages.empty()) {  // normalization-only chain: keep one empty stage record

@@ -31,6 +31,10 @@ constexpr int kSingleStageCap = 64 * 1024; // a whole chain this small lives in 
 constexpr int kStageAlign = 1024;          // one global->LDS DMA wave instruction (64 lanes x 16 B)
 constexpr int kMaxTableInts = 4096;  // 16 KiB of int32 tables in LDS
 constexpr int kMaxTilesPerWave = 8;          // 16-sample tiles per wave resident in LDS
+#ifndef DF_UNI_TT
+#define DF_UNI_TT 1
+#endif
+constexpr int kUniformTileGroup = DF_UNI_TT;  // tiles the specialised kernel evaluates together
 constexpr int kLdsPerBlockTarget = 80 * 1024; // two workgroups per CU
 
 enum : int32_t { IN_STATE = 0, IN_HIDDEN = 1 };

@@ -7,6 +7,8 @@
 // accumulators instead of register copies, compact per-net descriptors.
 #pragma once
 
+#include <type_traits>
+
 #include "df_chain_impl.h"
 
 namespace df {
@@ -17,16 +19,35 @@ using impl::lds4;
 using impl::mfma4;
 using impl::Stager;
 
-__device__ __forceinline__ float relu_fast(float x) { return __builtin_fmaxf(x, 0.f); }
+// relu(x) = max(0, x) as ONE v_max_i32 on the bit pattern: non-negative floats
+// order like their integer images; negative floats (and -0) map to +0; a NaN
+// with the sign bit clear (the canonical quiet NaN) propagates as in Julia.
+__device__ __forceinline__ float relu_fast(float x) {
+    return __int_as_float(__builtin_elementwise_max(__float_as_int(x), 0));
+}
 
-// acc = W·x (+ b), x = the state features vcat(θ,z)[axis_nn] (<= 16 of them).
-template <int HT>
-__device__ __forceinline__ void dense_first(const uint8_t* buf, const UNet& N, const float (&xin)[4],
-                                            f32x4 (&acc)[HT]) {
+// Σ over the 4 lane groups of a wave (lanes l, l^16, l^32, l^48) without LDS:
+// gfx950 v_permlane16_swap / v_permlane32_swap.  Every lane gets the bitwise
+// identical total ((p0+p1)+(p2+p3), commutations only).
+__device__ __forceinline__ float xgroup_sum(float p) {
+    auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(p), __float_as_uint(p), false, false);
+    const float q = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(q), __float_as_uint(q), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+constexpr int kTT = kUniformTileGroup;  // 16-sample tiles evaluated together in registers
+
+// acc = W·x, x = the state features vcat(θ,z)[axis_nn] (<= 16 of them).
+template <int HT, int TT>
+__device__ __forceinline__ void dense_first(const uint8_t* buf, const UNet& N, const float (&xin)[TT][4],
+                                            f32x4 (&acc)[TT][HT]) {
     const int lane = threadIdx.x & 63;
     const uint8_t* wb = buf + N.off_w0 + lane * 16;
 #pragma unroll
-    for (int m = 0; m < HT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int m = 0; m < HT; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 w[HT];
 #pragma unroll
     for (int m = 0; m < HT; ++m) w[m] = lds4(wb + m * 1024);
@@ -34,19 +55,23 @@ __device__ __forceinline__ void dense_first(const uint8_t* buf, const UNet& N, c
     for (int r = 0; r < 4; ++r) {
         if (r < N.ks) {
 #pragma unroll
-            for (int m = 0; m < HT; ++m) acc[m] = mfma4(w[m][r], xin[r], acc[m]);
+            for (int m = 0; m < HT; ++m)
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t][m] = mfma4(w[m][r], xin[t][r], acc[t][m]);
         }
     }
 }
 
 // out = W·in over a full H×H Dense (fragments [kq][m][lane][4] at wb).
-template <int HT>
-__device__ __forceinline__ void dense_hidden(const uint8_t* wb, const f32x4 (&in)[HT], f32x4 (&out)[HT]) {
+template <int HT, int TT>
+__device__ __forceinline__ void dense_hidden(const uint8_t* wb, const f32x4 (&in)[TT][HT], f32x4 (&out)[TT][HT]) {
     const int lane = threadIdx.x & 63;
     wb += lane * 16;
     constexpr int MB = HT < 4 ? HT : 4;
 #pragma unroll
-    for (int m = 0; m < HT; ++m) out[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int m = 0; m < HT; ++m) out[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int m0 = 0; m0 < HT; m0 += MB) {
         f32x4 w[2][MB];
@@ -62,174 +87,235 @@ __device__ __forceinline__ void dense_hidden(const uint8_t* wb, const f32x4 (&in
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int mm = 0; mm < MB; ++mm) out[m0 + mm] = mfma4(w[cb][mm][r], in[kq][r], out[m0 + mm]);
+                for (int mm = 0; mm < MB; ++mm)
+#pragma unroll
+                    for (int t = 0; t < TT; ++t)
+                        out[t][m0 + mm] = mfma4(w[cb][mm][r], in[t][kq][r], out[t][m0 + mm]);
         }
     }
 }
 
 // v = σ.(v .+ b)  — bias after the product (Flux: W*x .+ b)
-template <int HT>
-__device__ __forceinline__ void bias_act(const uint8_t* bb, int act, f32x4 (&v)[HT]) {
+template <int HT, int TT>
+__device__ __forceinline__ void bias_act(const uint8_t* bb, int act, f32x4 (&v)[TT][HT]) {
     const int g = (threadIdx.x & 63) >> 4;
 #pragma unroll
-    for (int m = 0; m < HT; ++m) v[m] = v[m] + lds4(bb + ((16 * m + 4 * g) << 2));
+    for (int m = 0; m < HT; ++m) {
+        const f32x4 b = lds4(bb + ((16 * m + 4 * g) << 2));
+#pragma unroll
+        for (int t = 0; t < TT; ++t) v[t][m] = v[t][m] + b;
+    }
     if (act == DF_ACT_RELU) {
 #pragma unroll
-        for (int m = 0; m < HT; ++m)
+        for (int t = 0; t < TT; ++t)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[m][r] = relu_fast(v[m][r]);
+            for (int m = 0; m < HT; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[t][m][r] = relu_fast(v[t][m][r]);
     } else if (act != DF_ACT_IDENTITY) {
 #pragma unroll
-        for (int m = 0; m < HT; ++m)
+        for (int t = 0; t < TT; ++t)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[m][r] = impl::act_fn(act, v[m][r]);
+            for (int m = 0; m < HT; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[t][m][r] = impl::act_fn(act, v[t][m][r]);
     }
 }
 
 // Final Dense, <= 4 outputs, as a VALU GEMV; every lane ends with all outputs.
-template <int HT>
-__device__ __forceinline__ f32x4 out_valu(const uint8_t* buf, const UNet& N, const f32x4 (&h)[HT]) {
+template <int HT, int TT>
+__device__ __forceinline__ void out_valu(const uint8_t* buf, const UNet& N, const f32x4 (&h)[TT][HT],
+                                         f32x4 (&o)[TT]) {
     const int g = (threadIdx.x & 63) >> 4;
     const uint8_t* w3 = buf + N.off_out;
     constexpr int INP = 16 * HT;
     const float* b3 = reinterpret_cast<const float*>(w3) + N.n_out * INP;
-    f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < TT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int oo = 0; oo < 4; ++oo) {
         if (oo < N.n_out) {
-            float p = 0.f;
+            float p[TT];
+#pragma unroll
+            for (int t = 0; t < TT; ++t) p[t] = 0.f;
 #pragma unroll
             for (int kq = 0; kq < HT; ++kq) {
                 const f32x4 w = lds4(w3 + ((oo * INP + 16 * kq + 4 * g) << 2));
 #pragma unroll
-                for (int r = 0; r < 4; ++r) p = __builtin_fmaf(w[r], h[kq][r], p);
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int t = 0; t < TT; ++t) p[t] = __builtin_fmaf(w[r], h[t][kq][r], p[t]);
             }
-            p += __shfl_xor(p, 16);
-            p += __shfl_xor(p, 32);
-            float v = p + b3[oo];
-            o[oo] = (N.act_out == DF_ACT_IDENTITY) ? v : impl::act_fn(N.act_out, v);
+            const float bo = b3[oo];
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                const float v = xgroup_sum(p[t]) + bo;
+                o[t][oo] = (N.act_out == DF_ACT_IDENTITY) ? v : impl::act_fn(N.act_out, v);
+            }
         }
     }
-    return o;
 }
 
-// Final Dense through MFMA (out <= 32): rows 16m + 4g + r in out[m].
-template <int HT>
-__device__ __forceinline__ void out_mfma(const uint8_t* buf, const UNet& N, const f32x4 (&h)[HT],
-                                         f32x4 (&out)[2]) {
+// Final Dense through MFMA (out <= 32): rows 16m + 4g + r in out[t][m].
+template <int HT, int TT>
+__device__ __forceinline__ void out_mfma(const uint8_t* buf, const UNet& N, const f32x4 (&h)[TT][HT],
+                                         f32x4 (&out)[TT][2]) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const uint8_t* wb = buf + N.off_out + lane * 16;
     const int mt = (N.n_out + 15) >> 4;
-    out[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    out[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < TT; ++t) out[t][0] = out[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kq = 0; kq < HT; ++kq) {
         const f32x4 w0 = lds4(wb + (kq * mt + 0) * 1024);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) out[0] = mfma4(w0[r], h[kq][r], out[0]);
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < TT; ++t) out[t][0] = mfma4(w0[r], h[t][kq][r], out[t][0]);
         if (mt > 1) {
             const f32x4 w1 = lds4(wb + (kq * mt + 1) * 1024);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) out[1] = mfma4(w1[r], h[kq][r], out[1]);
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int t = 0; t < TT; ++t) out[t][1] = mfma4(w1[r], h[t][kq][r], out[t][1]);
         }
     }
     const uint8_t* bb = buf + N.off_out + HT * mt * 1024;
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
         if (m < mt) {
-            f32x4 v = out[m] + lds4(bb + ((16 * m + 4 * g) << 2));
-            if (N.act_out != DF_ACT_IDENTITY)
+            const f32x4 b = lds4(bb + ((16 * m + 4 * g) << 2));
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = impl::act_fn(N.act_out, v[r]);
-            out[m] = v;
+            for (int t = 0; t < TT; ++t) {
+                f32x4 v = out[t][m] + b;
+                if (N.act_out != DF_ACT_IDENTITY)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = impl::act_fn(N.act_out, v[r]);
+                out[t][m] = v;
+            }
         }
     }
 }
 
-// Evaluate net N for one 16-sample tile (state rows at `ro`) and apply its
-// coupling phase; returns Σ_k s_k for s phases (row order), 0 otherwise.
-template <int HT, bool OUTV, int PH>
-__device__ __forceinline__ float net_tile(const uint8_t* buf, const UNet& N, const ULayer& L, const int32_t* tab,
-                                          float* state, int ro) {
+template <int PH>
+__device__ __forceinline__ float couple1(float v, float y) {
+    if (PH == impl::PH_S_FWD) return v * expf(y);
+    if (PH == impl::PH_T_FWD) return v + y;
+    if (PH == impl::PH_T_BWD) return v - y;
+    return v * expf(-y);  // PH_S_BWD
+}
+
+// Output Dense + coupling phase of net N on the last hidden activations H.
+template <int HT, int TT, bool OUTV, int PH>
+__device__ __forceinline__ void tail(const uint8_t* buf, const UNet& N, const ULayer& L, const int32_t* tab,
+                                     float* state, const int (&ro)[TT], float (&sum)[TT], const f32x4 (&H)[TT][HT]) {
+    const int g = (threadIdx.x & 63) >> 4;
+    constexpr bool SPH = (PH == impl::PH_S_FWD || PH == impl::PH_S_BWD);
+    const int32_t* af = tab + L.af_tab;
+#pragma unroll
+    for (int t = 0; t < TT; ++t) sum[t] = 0.f;
+#ifdef DF_EXP_NOTAIL  // diagnostic build only: no output Dense / coupling (results are wrong)
+    if (true) {
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            float acc = 0.f;
+#pragma unroll
+            for (int m = 0; m < HT; ++m) acc += H[t][m][0];
+            asm volatile("" ::"v"(acc));
+        }
+        return;
+    }
+#endif
+    if constexpr (OUTV) {
+        f32x4 o[TT];
+        out_valu<HT, TT>(buf, N, H, o);
+        const int slot = (g < L.n_af) ? af[g] : 0;
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            const float y = impl::sel4(o[t], g);
+            if (g < L.n_af) state[ro[t] + slot] = couple1<PH>(state[ro[t] + slot], y);
+            if (SPH) {
+                // ldj = Σ_k s[k] in row order (RNVP.jl:180 / :86)
+                float s_ = o[t][0];
+#pragma unroll
+                for (int oo = 1; oo < 4; ++oo)
+                    if (oo < L.n_af) s_ = s_ + o[t][oo];
+                sum[t] = s_;
+            }
+        }
+    } else {
+        f32x4 o[TT][2];
+        out_mfma<HT, TT>(buf, N, H, o);
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            float p = 0.f;
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int oo = 16 * m + 4 * g + r;
+                    if (oo < L.n_af) {
+                        const int slot = af[oo];
+                        const float y = o[t][m][r];
+                        state[ro[t] + slot] = couple1<PH>(state[ro[t] + slot], y);
+                        if (SPH) p = p + y;
+                    }
+                }
+            if (SPH) sum[t] = xgroup_sum(p);
+        }
+    }
+}
+
+// Evaluate net N for TT 16-sample tiles (state rows ro[t]) and apply its
+// coupling phase; sum[t] = Σ_k s_k for s phases (row order).
+template <int HT, int TT, bool OUTV, int PH>
+__device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, const ULayer& L, const int32_t* tab,
+                                          float* state, const int (&ro)[TT], float (&sum)[TT]) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
     constexpr bool SPH = (PH == impl::PH_S_FWD || PH == impl::PH_S_BWD);
     // conditioner input: features k = 4r + g of vcat(θ,z)[axis_nn] (zero slot pads)
-    float xin[4];
+    float xin[TT][4];
     const int32_t* feat = tab + L.feat_tab;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) xin[r] = (r < N.ks) ? state[ro + feat[4 * r + g]] : 0.f;
+    for (int r = 0; r < 4; ++r) {
+        const int slot = (r < N.ks) ? feat[4 * r + g] : 0;
+#pragma unroll
+        for (int t = 0; t < TT; ++t) xin[t][r] = (r < N.ks) ? state[ro[t] + slot] : 0.f;
+    }
 
-    f32x4 A[HT], B[HT];
-    dense_first<HT>(buf, N, xin, A);
-    bias_act<HT>(buf + N.off_b0, N.act0, A);
+    f32x4 A[TT][HT], B[TT][HT];
+    dense_first<HT, TT>(buf, N, xin, A);
+    bias_act<HT, TT>(buf + N.off_b0, N.act0, A);
+    if (N.nh == 1) {  // the default _dflt_net (n_sublayers = 2): one H×H Dense
+        dense_hidden<HT, TT>(buf + N.off_h, A, B);
+        bias_act<HT, TT>(buf + N.off_h + HT * HT * 1024, N.acth, B);
+        tail<HT, TT, OUTV, PH>(buf, N, L, tab, state, ro, sum, B);
+        return;
+    }
     // hidden Denses alternate A -> B -> A ... (no register copies)
     bool in_a = true;
     for (int k = 0; k < N.nh; k += 2) {
-        dense_hidden<HT>(buf + N.off_h + k * N.hstride, A, B);
-        bias_act<HT>(buf + N.off_h + k * N.hstride + HT * HT * 1024, N.acth, B);
+        dense_hidden<HT, TT>(buf + N.off_h + k * N.hstride, A, B);
+        bias_act<HT, TT>(buf + N.off_h + k * N.hstride + HT * HT * 1024, N.acth, B);
         in_a = false;
         if (k + 1 < N.nh) {
-            dense_hidden<HT>(buf + N.off_h + (k + 1) * N.hstride, B, A);
-            bias_act<HT>(buf + N.off_h + (k + 1) * N.hstride + HT * HT * 1024, N.acth, A);
+            dense_hidden<HT, TT>(buf + N.off_h + (k + 1) * N.hstride, B, A);
+            bias_act<HT, TT>(buf + N.off_h + (k + 1) * N.hstride + HT * HT * 1024, N.acth, A);
             in_a = true;
         }
     }
-    const int32_t* af = tab + L.af_tab;
-    float sum = 0.f;
-    if constexpr (OUTV) {
-        const f32x4 o = in_a ? out_valu<HT>(buf, N, A) : out_valu<HT>(buf, N, B);
-        const float y = impl::sel4(o, g);
-        if (g < L.n_af) {
-            const int slot = af[g];
-            float v = state[ro + slot];
-            if (PH == impl::PH_S_FWD) v = v * expf(y);
-            if (PH == impl::PH_T_FWD) v = v + y;
-            if (PH == impl::PH_T_BWD) v = v - y;
-            if (PH == impl::PH_S_BWD) v = v * expf(-y);
-            state[ro + slot] = v;
-        }
-        if (SPH) {
-            // ldj = Σ_k s[k] in row order (RNVP.jl:180 / :86)
-            sum = o[0];
-#pragma unroll
-            for (int oo = 1; oo < 4; ++oo)
-                if (oo < L.n_af) sum = sum + o[oo];
-        }
-    } else {
-        f32x4 o[2];
-        if (in_a) out_mfma<HT>(buf, N, A, o);
-        else out_mfma<HT>(buf, N, B, o);
-        float p = 0.f;
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int oo = 16 * m + 4 * g + r;
-                if (oo < L.n_af) {
-                    const int slot = af[oo];
-                    const float y = o[m][r];
-                    float v = state[ro + slot];
-                    if (PH == impl::PH_S_FWD) v = v * expf(y);
-                    if (PH == impl::PH_T_FWD) v = v + y;
-                    if (PH == impl::PH_T_BWD) v = v - y;
-                    if (PH == impl::PH_S_BWD) v = v * expf(-y);
-                    state[ro + slot] = v;
-                    if (SPH) p = p + y;
-                }
-            }
-        if (SPH) {
-            p += __shfl_xor(p, 16);
-            p += __shfl_xor(p, 32);
-            sum = p;
-        }
-    }
-    return sum;
+    if (in_a) tail<HT, TT, OUTV, PH>(buf, N, L, tab, state, ro, sum, A);
+    else tail<HT, TT, OUTV, PH>(buf, N, L, tab, state, ro, sum, B);
 }
 
 }  // namespace uni
 
+#ifndef DF_UNI_WAVES
+#define DF_UNI_WAVES 4
+#endif
+
 template <int HT, int MODE, bool OUTV>
-__global__ void __launch_bounds__(kBlockThreads, DF_WAVES_PER_EU(HT))
+__global__ void __launch_bounds__(kBlockThreads, DF_UNI_WAVES)
 uniform_kernel(ChainArgs a) {
     using namespace uni;
     constexpr bool FWD = (MODE == MODE_FWD || MODE == MODE_FWD_INPLACE);
@@ -314,40 +400,34 @@ uniform_kernel(ChainArgs a) {
             }
         } else {
             const bool rnvp = (kind == DF_LAYER_RNVP);
+            // this wave's tiles in groups of kTT (nt is a multiple of kTT)
+            auto run_net = [&](const UNet& N, auto ph_tag, bool sphase, float sign) {
+                constexpr int PH = decltype(ph_tag)::value;
+                impl::ensure_stage(N.stage, sg, a);
+                const uint8_t* buf = sg.buf();
+                for (int tt = 0; tt < nt; tt += kTT) {
+                    int ro[kTT];
+                    float ssum[kTT];
+#pragma unroll
+                    for (int t = 0; t < kTT; ++t) ro[t] = row0 + (tt + t) * tstep;
+                    net_tiles<HT, kTT, OUTV, PH>(buf, N, L, tab, state, ro, ssum);
+#pragma unroll
+                    for (int t = 0; t < kTT; ++t) {
+                        if (sphase) ldj_update(ro[t], sign * ssum[t], first_in_elem, last_in_elem);
+                        else if (!rnvp) ldj_update(ro[t], 0.f, first_in_elem, last_in_elem);
+                    }
+                }
+            };
+            using PSF = std::integral_constant<int, impl::PH_S_FWD>;
+            using PTF = std::integral_constant<int, impl::PH_T_FWD>;
+            using PTB = std::integral_constant<int, impl::PH_T_BWD>;
+            using PSB = std::integral_constant<int, impl::PH_S_BWD>;
             if (FWD) {
-                if (rnvp) {
-                    impl::ensure_stage(L.s.stage, sg, a);
-                    const uint8_t* buf = sg.buf();
-                    for (int tt = 0; tt < nt; ++tt) {
-                        const int ro = row0 + tt * tstep;
-                        const float ss = net_tile<HT, OUTV, impl::PH_S_FWD>(buf, L.s, L, tab, state, ro);
-                        ldj_update(ro, ss, first_in_elem, last_in_elem);
-                    }
-                }
-                impl::ensure_stage(L.t.stage, sg, a);
-                const uint8_t* buf = sg.buf();
-                for (int tt = 0; tt < nt; ++tt) {
-                    const int ro = row0 + tt * tstep;
-                    net_tile<HT, OUTV, impl::PH_T_FWD>(buf, L.t, L, tab, state, ro);
-                    if (!rnvp) ldj_update(ro, 0.f, first_in_elem, last_in_elem);
-                }
+                if (rnvp) run_net(L.s, PSF{}, true, 1.f);
+                run_net(L.t, PTF{}, false, 1.f);
             } else {
-                impl::ensure_stage(L.t.stage, sg, a);
-                const uint8_t* buf = sg.buf();
-                for (int tt = 0; tt < nt; ++tt) {
-                    const int ro = row0 + tt * tstep;
-                    net_tile<HT, OUTV, impl::PH_T_BWD>(buf, L.t, L, tab, state, ro);
-                    if (!rnvp) ldj_update(ro, 0.f, first_in_elem, last_in_elem);
-                }
-                if (rnvp) {
-                    impl::ensure_stage(L.s.stage, sg, a);
-                    const uint8_t* bs = sg.buf();
-                    for (int tt = 0; tt < nt; ++tt) {
-                        const int ro = row0 + tt * tstep;
-                        const float ss = net_tile<HT, OUTV, impl::PH_S_BWD>(bs, L.s, L, tab, state, ro);
-                        ldj_update(ro, -ss, first_in_elem, last_in_elem);  // ln_det_jac = -Σ s
-                    }
-                }
+                run_net(L.t, PTB{}, false, 1.f);
+                if (rnvp) run_net(L.s, PSB{}, true, -1.f);  // ln_det_jac = -Σ s
             }
         }
         have_acc = have_acc || last_in_elem;
