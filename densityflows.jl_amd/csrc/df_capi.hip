@@ -83,6 +83,8 @@ struct df_chain {
     size_t lds = 0;
 };
 
+static int uniform_variant(const df::Plan& P) { return P.uniform ? (P.relu_only ? 2 : 1) : 0; }
+
 static size_t lds_for_tiles(const df_chain* c, int t) {
     const df::Plan& P = c->plan;
     return (size_t)c->stage_bytes * c->n_stage_bufs + c->tab_bytes +
@@ -151,11 +153,6 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
         delete c;
         return set_err(rc, err);
     }
-    if (const char* f = std::getenv("DF_FORCE_GENERIC"))  // A/B switch for testing the generic kernel
-        if (f[0] == '1') {
-            c->plan.uniform = 0;
-            c->plan.ulayers.clear();
-        }
     c->device = device;
     DeviceGuard gd(device);
     if (!gd.ok) {
@@ -201,7 +198,7 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
     for (int mode = 0; mode < 4; ++mode)
         for (int t = 1; t <= P.tiles; ++t) {
             int blocks = 1;
-            if (df::kernel_occupancy(P.ht, mode, P.outv != 0, P.uniform != 0, lds_for_tiles(c, t), &blocks) !=
+            if (df::kernel_occupancy(P.ht, mode, P.outv != 0, uniform_variant(P), lds_for_tiles(c, t), &blocks) !=
                     hipSuccess ||
                 blocks < 1)
                 blocks = 1;
@@ -329,7 +326,7 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     a.c0 = -((float)P.d * (float)kLog2Pi + 0.f) / 2.f;
 
     hipStream_t st = static_cast<hipStream_t>(stream);
-    hipError_t e = df::launch_chain(P.ht, mode, P.outv != 0, P.uniform != 0, a, (unsigned)grid,
+    hipError_t e = df::launch_chain(P.ht, mode, P.outv != 0, uniform_variant(P), a, (unsigned)grid,
                                     lds_for_tiles(c, tiles), st);
     if (e != hipSuccess) return hip_err(e, "chain kernel launch");
     if (sum_out) {

@@ -43,12 +43,13 @@ hipError_t set_kernel_lds_limit(int ht, bool uniform, size_t lds) {
     }
 }
 
-hipError_t kernel_occupancy(int ht, int mode, bool outv, bool uniform, size_t lds, int* blocks) {
+hipError_t kernel_occupancy(int ht, int mode, bool outv, int uniform, size_t lds, int* blocks) {
     if (uniform) {
+        const int v = (outv ? 1 : 0) | (uniform == 2 ? 2 : 0);
         switch (ht) {
-            case 1: return uniform_occupancy_ht<1>(mode, outv, lds, blocks);
-            case 2: return uniform_occupancy_ht<2>(mode, outv, lds, blocks);
-            case 4: return uniform_occupancy_ht<4>(mode, outv, lds, blocks);
+            case 1: return uniform_occupancy_ht<1>(mode, v, lds, blocks);
+            case 2: return uniform_occupancy_ht<2>(mode, v, lds, blocks);
+            case 4: return uniform_occupancy_ht<4>(mode, v, lds, blocks);
             default: return hipErrorInvalidValue;
         }
     }
@@ -62,13 +63,14 @@ hipError_t kernel_occupancy(int ht, int mode, bool outv, bool uniform, size_t ld
     }
 }
 
-hipError_t launch_chain(int ht, int mode, bool outv, bool uniform, const ChainArgs& a, unsigned grid, size_t lds,
+hipError_t launch_chain(int ht, int mode, bool outv, int uniform, const ChainArgs& a, unsigned grid, size_t lds,
                         hipStream_t st) {
     if (uniform) {
+        const int v = (outv ? 1 : 0) | (uniform == 2 ? 2 : 0);
         switch (ht) {
-            case 1: return launch_uniform_ht<1>(mode, outv, a, grid, lds, st);
-            case 2: return launch_uniform_ht<2>(mode, outv, a, grid, lds, st);
-            case 4: return launch_uniform_ht<4>(mode, outv, a, grid, lds, st);
+            case 1: return launch_uniform_ht<1>(mode, v, a, grid, lds, st);
+            case 2: return launch_uniform_ht<2>(mode, v, a, grid, lds, st);
+            case 4: return launch_uniform_ht<4>(mode, v, a, grid, lds, st);
             default: return hipErrorInvalidValue;
         }
     }

@@ -51,19 +51,20 @@ hipError_t launch_chain_ht(int mode, bool outv, const ChainArgs& a, unsigned gri
 template <int HT>
 hipError_t set_lds_limit_ht(size_t lds);
 template <int HT>
-hipError_t launch_uniform_ht(int mode, bool outv, const ChainArgs& a, unsigned grid, size_t lds, hipStream_t st);
+hipError_t launch_uniform_ht(int mode, int variant, const ChainArgs& a, unsigned grid, size_t lds, hipStream_t st);
 template <int HT>
 hipError_t set_uniform_lds_limit_ht(size_t lds);
 template <int HT>
-hipError_t uniform_occupancy_ht(int mode, bool outv, size_t lds, int* blocks);
+hipError_t uniform_occupancy_ht(int mode, int variant, size_t lds, int* blocks);
 template <int HT>
 hipError_t chain_occupancy_ht(int mode, bool outv, size_t lds, int* blocks);
 
 // Dispatch over the variant (df_common.hip).
 hipError_t set_kernel_lds_limit(int ht, bool uniform, size_t lds);
-hipError_t launch_chain(int ht, int mode, bool outv, bool uniform, const ChainArgs& a, unsigned grid,
+// uniform: 0 = generic kernel, 1 = specialised, 2 = specialised relu-only
+hipError_t launch_chain(int ht, int mode, bool outv, int uniform, const ChainArgs& a, unsigned grid,
                         size_t lds, hipStream_t st);
-hipError_t kernel_occupancy(int ht, int mode, bool outv, bool uniform, size_t lds, int* blocks);
+hipError_t kernel_occupancy(int ht, int mode, bool outv, int uniform, size_t lds, int* blocks);
 hipError_t launch_reduce_partials(const double* part, int64_t n, double* out, hipStream_t st);
 
 }  // namespace df

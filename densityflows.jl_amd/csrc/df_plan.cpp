@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
 #include <set>
 #include <sstream>
 
@@ -200,6 +201,32 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
         P.ht = pow2_tiles(max_tiles);
         if (P.ht > kMaxHidden / 16) fail(DF_ERR_UNSUPPORTED, "hidden width > 256");
 
+        // ---------- pass 1b: does every net have the default _dflt_net shape? ----------
+        // Dense(in<=16, H) -> nh × Dense(H, H) -> Dense(H, out) with ceil(H/16) = HT <= 4,
+        // one hidden σ per net.  Such chains run on the specialised kernel, whose
+        // first Dense uses a compact fragment layout (no k-quad padding).
+        bool uniform_shape = P.ht <= 4;
+        bool relu_only = true;
+        if (const char* f = std::getenv("DF_FORCE_GENERIC"))
+            if (f[0] == '1') uniform_shape = false;
+        for (int li = 0; li < desc->n_layers && uniform_shape; ++li) {
+            const df_layer_desc& L = desc->layers[li];
+            if (L.kind == DF_LAYER_NORM) continue;
+            auto ok_net = [&](const df_dense_desc* net, int nd) {
+                if (nd < 2 || (L.n_nn + 3) / 4 > 4) return false;
+                for (int k = 0; k + 1 < nd; ++k) {
+                    if ((net[k].out_dim + 15) / 16 != P.ht) return false;
+                    if (k >= 1 && net[k].act != net[1].act) return false;
+                    if (net[k].act != DF_ACT_RELU) relu_only = false;
+                }
+                if (net[nd - 1].act != DF_ACT_IDENTITY) relu_only = false;
+                if (!all_valu && (net[nd - 1].out_dim + 15) / 16 > 2) return false;
+                return true;
+            };
+            if (L.kind == DF_LAYER_RNVP) uniform_shape = uniform_shape && ok_net(L.s_net, L.n_dense_s);
+            uniform_shape = uniform_shape && ok_net(L.t_net, L.n_dense_t);
+        }
+
         // ---------- pass 2: packing ----------
         // Whole chain in one stage when it is small (loaded once per workgroup);
         // otherwise 24 KiB stages, double-buffered in LDS, one net per stage
@@ -218,7 +245,8 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                     } else {
                         const int mt = (net[k].out_dim + 15) / 16;
                         const int ks = (k == 0) ? (L.n_nn + 3) / 4 : 4 * prev_tiles;
-                        b += (int64_t)((ks + 3) / 4) * mt * 1024 + mt * 64;
+                        if (k == 0 && uniform_shape) b += (int64_t)mt * ks * 256 + mt * 64;
+                        else b += (int64_t)((ks + 3) / 4) * mt * 1024 + mt * 64;
                         prev_tiles = mt;
                     }
                 }
@@ -295,6 +323,10 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                     P.denses.push_back(DD);
                     if (DD.out_valu) {
                         items.push_back({Item::W3, idx, 0, round_up((D.out_dim * 16 * DD.kt_in + 4) * 4, 16)});
+                    } else if (DD.in_kind == IN_STATE && uniform_shape) {
+                        P.denses[idx].compact = 1;
+                        items.push_back({Item::CHUNK_KQ, idx, 0, round_up(DD.mt * DD.ks * 256, 16)});
+                        items.push_back({Item::BIAS, idx, 0, DD.mt * 16 * 4});
                     } else {
                         int nkq = (DD.ks + 3) / 4;
                         for (int kq = 0; kq < nkq; ++kq) items.push_back({Item::CHUNK_KQ, idx, kq, DD.mt * 1024});
@@ -330,7 +362,7 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
             for (size_t ii = 0; ii < items.size(); ++ii) {
                 const Item& it = items[ii];
                 const bool net_start = (ii == 0) || ((items[ii - 1].dense >= t_first_dense) != (it.dense >= t_first_dense));
-                if (net_start && ii > 0) {
+                if (net_start) {
                     const int nb = net_bytes_from(ii);
                     if (nb > pk.remaining() && nb <= pk.cap()) pk.begin_stage();
                 }
@@ -357,6 +389,13 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                         DD.chunk0 = (int)P.chunks.size();
                         P.chunks.push_back({st, off, it.kq, it.kq + 1});
                         DD.n_chunks = 1;
+                    }
+                    if (DD.compact) {  // [m][r < ks][lane]: k = 4r + g
+                        for (int m = 0; m < DD.mt; ++m)
+                            for (int r = 0; r < DD.ks; ++r)
+                                for (int lane = 0; lane < 64; ++lane)
+                                    dst[(m * DD.ks + r) * 64 + lane] = W(16 * m + (lane & 15), 4 * r + (lane >> 4));
+                        continue;
                     }
                     // fragment [m][lane][r] for k-quad kq
                     for (int m = 0; m < DD.mt; ++m)
@@ -460,11 +499,13 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
             resident = resident && one_stage(L.s_dense0, L.s_ndense) && one_stage(L.t_dense0, L.t_ndense);
         }
         // Specialised-kernel descriptors when every net has the default shape.
-        P.uniform = (resident && P.ht <= 4) ? 1 : 0;
+        P.uniform = (uniform_shape && resident) ? 1 : 0;
+        P.relu_only = (P.uniform && relu_only) ? 1 : 0;
+        if (uniform_shape && !resident) fail(DF_ERR_UNSUPPORTED, "internal: default-shape net split across stages");
         auto make_unet = [&](int d0, int nd, UNet* u) -> bool {
             if (nd < 2) return false;
             const DevDense& D0 = P.denses[d0];
-            if (D0.in_kind != IN_STATE || D0.ks > 4 || D0.mt != P.ht || D0.n_chunks != 1) return false;
+            if (D0.in_kind != IN_STATE || D0.ks > 4 || D0.mt != P.ht || D0.n_chunks != 1 || !D0.compact) return false;
             const DevChunk& C0 = P.chunks[D0.chunk0];
             u->stage = C0.stage;
             u->ks = D0.ks;
@@ -519,10 +560,7 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                 if (L.kind != DF_LAYER_NORM) {
                     bool ok = make_unet(L.t_dense0, L.t_ndense, &U.t);
                     if (L.kind == DF_LAYER_RNVP) ok = ok && make_unet(L.s_dense0, L.s_ndense, &U.s);
-                    if (!ok) {
-                        P.uniform = 0;
-                        break;
-                    }
+                    if (!ok) fail(DF_ERR_UNSUPPORTED, "internal: default-shape net with an irregular layout");
                 }
                 P.ulayers.push_back(U);
             }
@@ -536,12 +574,8 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
         if (resident)
             while (P.tiles < kMaxTilesPerWave && fixed + (P.tiles + 1) * per_tile <= kLdsPerBlockTarget) ++P.tiles;
         if (P.uniform) {  // the specialised kernel evaluates tiles in groups
-            if (P.tiles < kUniformTileGroup) {
-                P.uniform = 0;
-                P.ulayers.clear();
-            } else {
-                P.tiles -= P.tiles % kUniformTileGroup;
-            }
+            if (P.tiles < kUniformTileGroup) fail(DF_ERR_UNSUPPORTED, "LDS too small for the specialised kernel");
+            P.tiles -= P.tiles % kUniformTileGroup;
         }
         P.samples_per_block = kWavesPerBlock * 16 * P.tiles;
         if ((int)P.tables.size() > kMaxTableInts) fail(DF_ERR_UNSUPPORTED, "chain index tables exceed 16 KiB");

@@ -57,7 +57,8 @@ struct DevDense {
     int32_t bias_stage, bias_lds;  // bias padded to 16*mt floats (MFMA path)
     int32_t chunk0, n_chunks;
     int32_t w3_stage, w3_lds;      // VALU path: W [n_out][16*kt_in] row-major, then b[4]
-    int32_t pad0, pad1;
+    int32_t compact;               // IN_STATE, specialised kernel: [m][r < ks][lane] f32 (no k-quad padding)
+    int32_t pad1;
 };
 
 struct DevLayer {
@@ -108,6 +109,7 @@ struct Plan {
     int tiles = 0;           // 16-sample tiles per wave resident in LDS
     int outv = 0;            // kernel variant: final Dense as VALU GEMV (<= 4 outputs)
     int uniform = 0;         // every layer fits the specialised kernel (ulayers valid)
+    int relu_only = 0;       // specialised kernel variant: hidden σ = relu, output σ = identity
     std::vector<ULayer> ulayers;
     int samples_per_block = 0;
     int stage_max = 0;       // largest stage (bytes, multiple of kStageAlign)

@@ -39,35 +39,39 @@ __device__ __forceinline__ float xgroup_sum(float p) {
 constexpr int kTT = kUniformTileGroup;  // 16-sample tiles evaluated together in registers
 
 // acc = W·x, x = the state features vcat(θ,z)[axis_nn] (<= 16 of them).
+// Compact fragments: [m][r < ks][lane] f32, k = 4r + lane_group.
 template <int HT, int TT>
 __device__ __forceinline__ void dense_first(const uint8_t* buf, const UNet& N, const float (&xin)[TT][4],
                                             f32x4 (&acc)[TT][HT]) {
     const int lane = threadIdx.x & 63;
-    const uint8_t* wb = buf + N.off_w0 + lane * 16;
+    const float* wb = reinterpret_cast<const float*>(buf + N.off_w0) + lane;
+    const int ks = N.ks;
 #pragma unroll
     for (int t = 0; t < TT; ++t)
 #pragma unroll
         for (int m = 0; m < HT; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 w[HT];
-#pragma unroll
-    for (int m = 0; m < HT; ++m) w[m] = lds4(wb + m * 1024);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        if (r < N.ks) {
+        if (r < ks) {
 #pragma unroll
-            for (int m = 0; m < HT; ++m)
+            for (int m = 0; m < HT; ++m) {
+                const float w = wb[(m * ks + r) * 64];
 #pragma unroll
-                for (int t = 0; t < TT; ++t) acc[t][m] = mfma4(w[m][r], xin[t][r], acc[t][m]);
+                for (int t = 0; t < TT; ++t) acc[t][m] = mfma4(w, xin[t][r], acc[t][m]);
+            }
         }
     }
 }
 
 // out = W·in over a full H×H Dense (fragments [kq][m][lane][4] at wb).
+// m-tiles are processed in pairs: two interleaved accumulator chains (64
+// cycles apart >= the 40-cycle MFMA dependency latency) and only 2×2
+// fragment registers in flight (next k-quad prefetched).
 template <int HT, int TT>
 __device__ __forceinline__ void dense_hidden(const uint8_t* wb, const f32x4 (&in)[TT][HT], f32x4 (&out)[TT][HT]) {
     const int lane = threadIdx.x & 63;
     wb += lane * 16;
-    constexpr int MB = HT < 4 ? HT : 4;
+    constexpr int MB = HT < 2 ? HT : 2;
 #pragma unroll
     for (int t = 0; t < TT; ++t)
 #pragma unroll
@@ -96,7 +100,7 @@ __device__ __forceinline__ void dense_hidden(const uint8_t* wb, const f32x4 (&in
 }
 
 // v = σ.(v .+ b)  — bias after the product (Flux: W*x .+ b)
-template <int HT, int TT>
+template <int HT, int TT, bool RELU>
 __device__ __forceinline__ void bias_act(const uint8_t* bb, int act, f32x4 (&v)[TT][HT]) {
     const int g = (threadIdx.x & 63) >> 4;
 #pragma unroll
@@ -105,7 +109,7 @@ __device__ __forceinline__ void bias_act(const uint8_t* bb, int act, f32x4 (&v)[
 #pragma unroll
         for (int t = 0; t < TT; ++t) v[t][m] = v[t][m] + b;
     }
-    if (act == DF_ACT_RELU) {
+    if (RELU || act == DF_ACT_RELU) {
 #pragma unroll
         for (int t = 0; t < TT; ++t)
 #pragma unroll
@@ -113,17 +117,19 @@ __device__ __forceinline__ void bias_act(const uint8_t* bb, int act, f32x4 (&v)[
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[t][m][r] = relu_fast(v[t][m][r]);
     } else if (act != DF_ACT_IDENTITY) {
+        if (!RELU) {
 #pragma unroll
-        for (int t = 0; t < TT; ++t)
+            for (int t = 0; t < TT; ++t)
 #pragma unroll
-            for (int m = 0; m < HT; ++m)
+                for (int m = 0; m < HT; ++m)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[t][m][r] = impl::act_fn(act, v[t][m][r]);
+                    for (int r = 0; r < 4; ++r) v[t][m][r] = impl::act_fn(act, v[t][m][r]);
+        }
     }
 }
 
 // Final Dense, <= 4 outputs, as a VALU GEMV; every lane ends with all outputs.
-template <int HT, int TT>
+template <int HT, int TT, bool RELU>
 __device__ __forceinline__ void out_valu(const uint8_t* buf, const UNet& N, const f32x4 (&h)[TT][HT],
                                          f32x4 (&o)[TT]) {
     const int g = (threadIdx.x & 63) >> 4;
@@ -150,14 +156,14 @@ __device__ __forceinline__ void out_valu(const uint8_t* buf, const UNet& N, cons
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
                 const float v = xgroup_sum(p[t]) + bo;
-                o[t][oo] = (N.act_out == DF_ACT_IDENTITY) ? v : impl::act_fn(N.act_out, v);
+                o[t][oo] = (RELU || N.act_out == DF_ACT_IDENTITY) ? v : impl::act_fn(N.act_out, v);
             }
         }
     }
 }
 
 // Final Dense through MFMA (out <= 32): rows 16m + 4g + r in out[t][m].
-template <int HT, int TT>
+template <int HT, int TT, bool RELU>
 __device__ __forceinline__ void out_mfma(const uint8_t* buf, const UNet& N, const f32x4 (&h)[TT][HT],
                                          f32x4 (&out)[TT][2]) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
@@ -188,7 +194,7 @@ __device__ __forceinline__ void out_mfma(const uint8_t* buf, const UNet& N, cons
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
                 f32x4 v = out[t][m] + b;
-                if (N.act_out != DF_ACT_IDENTITY)
+                if (!RELU && N.act_out != DF_ACT_IDENTITY)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) v[r] = impl::act_fn(N.act_out, v[r]);
                 out[t][m] = v;
@@ -206,7 +212,7 @@ __device__ __forceinline__ float couple1(float v, float y) {
 }
 
 // Output Dense + coupling phase of net N on the last hidden activations H.
-template <int HT, int TT, bool OUTV, int PH>
+template <int HT, int TT, bool OUTV, bool RELU, int PH>
 __device__ __forceinline__ void tail(const uint8_t* buf, const UNet& N, const ULayer& L, const int32_t* tab,
                                      float* state, const int (&ro)[TT], float (&sum)[TT], const f32x4 (&H)[TT][HT]) {
     const int g = (threadIdx.x & 63) >> 4;
@@ -228,7 +234,7 @@ __device__ __forceinline__ void tail(const uint8_t* buf, const UNet& N, const UL
 #endif
     if constexpr (OUTV) {
         f32x4 o[TT];
-        out_valu<HT, TT>(buf, N, H, o);
+        out_valu<HT, TT, RELU>(buf, N, H, o);
         const int slot = (g < L.n_af) ? af[g] : 0;
 #pragma unroll
         for (int t = 0; t < TT; ++t) {
@@ -245,7 +251,7 @@ __device__ __forceinline__ void tail(const uint8_t* buf, const UNet& N, const UL
         }
     } else {
         f32x4 o[TT][2];
-        out_mfma<HT, TT>(buf, N, H, o);
+        out_mfma<HT, TT, RELU>(buf, N, H, o);
 #pragma unroll
         for (int t = 0; t < TT; ++t) {
             float p = 0.f;
@@ -268,7 +274,7 @@ __device__ __forceinline__ void tail(const uint8_t* buf, const UNet& N, const UL
 
 // Evaluate net N for TT 16-sample tiles (state rows ro[t]) and apply its
 // coupling phase; sum[t] = Σ_k s_k for s phases (row order).
-template <int HT, int TT, bool OUTV, int PH>
+template <int HT, int TT, bool OUTV, bool RELU, int PH>
 __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, const ULayer& L, const int32_t* tab,
                                           float* state, const int (&ro)[TT], float (&sum)[TT]) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
@@ -285,27 +291,27 @@ __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, con
 
     f32x4 A[TT][HT], B[TT][HT];
     dense_first<HT, TT>(buf, N, xin, A);
-    bias_act<HT, TT>(buf + N.off_b0, N.act0, A);
+    bias_act<HT, TT, RELU>(buf + N.off_b0, N.act0, A);
     if (N.nh == 1) {  // the default _dflt_net (n_sublayers = 2): one H×H Dense
         dense_hidden<HT, TT>(buf + N.off_h, A, B);
-        bias_act<HT, TT>(buf + N.off_h + HT * HT * 1024, N.acth, B);
-        tail<HT, TT, OUTV, PH>(buf, N, L, tab, state, ro, sum, B);
+        bias_act<HT, TT, RELU>(buf + N.off_h + HT * HT * 1024, N.acth, B);
+        tail<HT, TT, OUTV, RELU, PH>(buf, N, L, tab, state, ro, sum, B);
         return;
     }
     // hidden Denses alternate A -> B -> A ... (no register copies)
     bool in_a = true;
     for (int k = 0; k < N.nh; k += 2) {
         dense_hidden<HT, TT>(buf + N.off_h + k * N.hstride, A, B);
-        bias_act<HT, TT>(buf + N.off_h + k * N.hstride + HT * HT * 1024, N.acth, B);
+        bias_act<HT, TT, RELU>(buf + N.off_h + k * N.hstride + HT * HT * 1024, N.acth, B);
         in_a = false;
         if (k + 1 < N.nh) {
             dense_hidden<HT, TT>(buf + N.off_h + (k + 1) * N.hstride, B, A);
-            bias_act<HT, TT>(buf + N.off_h + (k + 1) * N.hstride + HT * HT * 1024, N.acth, A);
+            bias_act<HT, TT, RELU>(buf + N.off_h + (k + 1) * N.hstride + HT * HT * 1024, N.acth, A);
             in_a = true;
         }
     }
-    if (in_a) tail<HT, TT, OUTV, PH>(buf, N, L, tab, state, ro, sum, A);
-    else tail<HT, TT, OUTV, PH>(buf, N, L, tab, state, ro, sum, B);
+    if (in_a) tail<HT, TT, OUTV, RELU, PH>(buf, N, L, tab, state, ro, sum, A);
+    else tail<HT, TT, OUTV, RELU, PH>(buf, N, L, tab, state, ro, sum, B);
 }
 
 }  // namespace uni
@@ -314,7 +320,7 @@ __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, con
 #define DF_UNI_WAVES 4
 #endif
 
-template <int HT, int MODE, bool OUTV>
+template <int HT, int MODE, bool OUTV, bool RELU>
 __global__ void __launch_bounds__(kBlockThreads, DF_UNI_WAVES)
 uniform_kernel(ChainArgs a) {
     using namespace uni;
@@ -410,7 +416,7 @@ uniform_kernel(ChainArgs a) {
                     float ssum[kTT];
 #pragma unroll
                     for (int t = 0; t < kTT; ++t) ro[t] = row0 + (tt + t) * tstep;
-                    net_tiles<HT, kTT, OUTV, PH>(buf, N, L, tab, state, ro, ssum);
+                    net_tiles<HT, kTT, OUTV, RELU, PH>(buf, N, L, tab, state, ro, ssum);
 #pragma unroll
                     for (int t = 0; t < kTT; ++t) {
                         if (sphase) ldj_update(ro[t], sign * ssum[t], first_in_elem, last_in_elem);
@@ -477,10 +483,10 @@ uniform_kernel(ChainArgs a) {
     }
 }
 
-template <int HT>
-void* uniform_kernel_ptr(int mode, bool outv) {
-#define DF_U(M) (outv ? reinterpret_cast<void*>(&uniform_kernel<HT, M, true>) \
-                      : reinterpret_cast<void*>(&uniform_kernel<HT, M, false>))
+template <int HT, bool RELU>
+void* uniform_kernel_ptr_r(int mode, bool outv) {
+#define DF_U(M) (outv ? reinterpret_cast<void*>(&uniform_kernel<HT, M, true, RELU>) \
+                      : reinterpret_cast<void*>(&uniform_kernel<HT, M, false, RELU>))
     switch (mode) {
         case MODE_FWD: return DF_U(MODE_FWD);
         case MODE_FWD_INPLACE: return DF_U(MODE_FWD_INPLACE);
@@ -490,17 +496,24 @@ void* uniform_kernel_ptr(int mode, bool outv) {
 #undef DF_U
 }
 
+// variant index: bit 0 = OUTV, bit 1 = RELU
 template <int HT>
-hipError_t launch_uniform_ht(int mode, bool outv, const ChainArgs& a, unsigned grid, size_t lds, hipStream_t st) {
+void* uniform_kernel_ptr(int mode, int variant) {
+    const bool outv = variant & 1;
+    return (variant & 2) ? uniform_kernel_ptr_r<HT, true>(mode, outv) : uniform_kernel_ptr_r<HT, false>(mode, outv);
+}
+
+template <int HT>
+hipError_t launch_uniform_ht(int mode, int variant, const ChainArgs& a, unsigned grid, size_t lds, hipStream_t st) {
     void* args[] = {const_cast<ChainArgs*>(&a)};
-    return hipLaunchKernel(uniform_kernel_ptr<HT>(mode, outv), dim3(grid), dim3(kBlockThreads), args, lds, st);
+    return hipLaunchKernel(uniform_kernel_ptr<HT>(mode, variant), dim3(grid), dim3(kBlockThreads), args, lds, st);
 }
 
 template <int HT>
 hipError_t set_uniform_lds_limit_ht(size_t lds) {
     for (int mode = 0; mode < 4; ++mode)
-        for (int ov = 0; ov < 2; ++ov) {
-            hipError_t e = hipFuncSetAttribute(uniform_kernel_ptr<HT>(mode, ov != 0),
+        for (int v = 0; v < 4; ++v) {
+            hipError_t e = hipFuncSetAttribute(uniform_kernel_ptr<HT>(mode, v),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
@@ -508,8 +521,8 @@ hipError_t set_uniform_lds_limit_ht(size_t lds) {
 }
 
 template <int HT>
-hipError_t uniform_occupancy_ht(int mode, bool outv, size_t lds, int* blocks) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, uniform_kernel_ptr<HT>(mode, outv), kBlockThreads,
+hipError_t uniform_occupancy_ht(int mode, int variant, size_t lds, int* blocks) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, uniform_kernel_ptr<HT>(mode, variant), kBlockThreads,
                                                         lds);
 }
 
