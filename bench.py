@@ -34,6 +34,22 @@ sys.path.insert(0, ROOT)
 METRIC = "forward+logdetJ Msamples/s, d=5 8-layer RealNVP, 1/2/4/8 MI355X"
 PEAK_F32_TFLOPS = 157.3   # MI355X f32 MFMA dense peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+# HBM bytes per launch of the headline kernel from rocprofv3 PMC counters
+# (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, WRITE_SIZE as is; KiB),
+# measured on the headline workload and committed under profiles/.
+TRAFFIC_PROFILE = os.path.join("profiles", "r01_v6_pmc_summary.txt")
+
+
+def pmc_traffic(path):
+    try:
+        vals = {}
+        for line in open(os.path.join(ROOT, path)):
+            parts = line.split()
+            if len(parts) == 2 and parts[0] in ("FETCH_SIZE", "WRITE_SIZE"):
+                vals[parts[0]] = float(parts[1].replace(",", ""))
+        return (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+    except Exception:
+        return None
 
 
 CONFIGS = {
@@ -134,20 +150,26 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)          # ranks share a device only in single-GPU rehearsals
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("DF_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import densityflows_amd as dfa
     from densityflows_amd.hip import HIPChain
 
     d, n, workload = CONFIGS[args.config]
     chain = build_chain(args.config)
-    hc = chain.hip(device=local, n_hint=n)
+    hc = chain.hip(device=gpu, n_hint=n)
     info = hc.info
     B = args.batch
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -162,7 +184,7 @@ def main():
             hc.run("forward", zbuf, thbuf, xbuf, ldj, B)
     else:
         flow = dfa.Flow(chain, metadata=dfa.MetaData("", d, n, np.zeros(n, np.float32), np.ones(n, np.float32)))
-        fh = flow.hip(device=local)
+        fh = flow.hip(device=gpu)
         hc.run("forward", zbuf, thbuf, xbuf, ldj, B)  # data points x = forward(z)
 
         def step():
@@ -201,6 +223,9 @@ def main():
     achieved_tflops = flop / kernel_s / 1e12
     hbm_algo = (8.0 * d + 4.0 * n + 4.0) * B          # read z (+θ), write x, ldj
 
+    traffic = None
+    if args.config == "cfg2" and args.mode == "forward" and B == (1 << 20):
+        traffic = pmc_traffic(TRAFFIC_PROFILE)
     if rank == 0:
         out = {
             "metric": METRIC if args.mode == "forward" else "NLL (inverse+logpdf+Σ, RCCL all-reduce) Msamples/s",
@@ -221,7 +246,8 @@ def main():
                        if args.mode == "forward" else f"dp{world} + RCCL all-reduce of the NLL partial"},
             "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": PEAK_F32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_F32_TFLOPS, 4),
-                         "traffic": None,
+                         "traffic": traffic,
+                         "traffic_source": TRAFFIC_PROFILE if traffic is not None else None,
                          "kernel_ms": round(kernel_s * 1e3, 4),
                          "algorithmic_flop_per_sample": info.flops_per_sample,
                          "hbm_algorithmic_GBps": round(hbm_algo / kernel_s / 1e9, 2)},
