@@ -17,6 +17,7 @@ from .flows import (Flow, MvNormal, logpdf, nll_partial_sum, pdf, predict, sampl
                     validation_loss)
 from .layers import (Chain, CouplingBlock, CouplingLayer, Dense, FlowElement, NICECouplingLayer,
                      NormalizationLayer, RNVPCouplingLayer, default_net)
+from .train import Adam, TrainState, load_trainables, setup, train_, trainables
 
 __version__ = "0.1.0"
 

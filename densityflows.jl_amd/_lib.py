@@ -88,6 +88,10 @@ class df_chain_info(C.Structure):
                 ("flops_per_sample", C.c_double), ("weight_bytes", C.c_int64)]
 
 
+class df_adam(C.Structure):
+    _fields_ = [("eta", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("epsilon", C.c_float)]
+
+
 _FP = C.POINTER(C.c_float)
 _VP = C.c_void_p
 _I64 = C.c_int64
@@ -110,6 +114,15 @@ SIGNATURES = {
     "df_flow_forward_inplace": (C.c_int, [_VP, _VP, _VP, _I64, _VP]),
     "df_flow_logpdf": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP]),
     "df_flow_logpdf_sum": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP]),
+    "df_train_create": (C.c_int, [C.POINTER(_VP), _VP, C.POINTER(df_adam)]),
+    "df_train_destroy": (C.c_int, [_VP]),
+    "df_train_num_params": (C.c_int, [_VP, C.POINTER(_I64)]),
+    "df_train_gradient": (C.c_int, [_VP, _VP, _VP, _I64, _I64, _VP, _VP]),
+    "df_train_grad_ptr": (C.c_int, [_VP, C.POINTER(_VP)]),
+    "df_train_apply": (C.c_int, [_VP, _VP]),
+    "df_train_step": (C.c_int, [_VP, _VP, _VP, _I64, _VP, _VP]),
+    "df_train_get_params": (C.c_int, [_VP, _FP, _I64]),
+    "df_train_set_params": (C.c_int, [_VP, _FP, _I64]),
     "df_device_alloc": (C.c_int, [C.POINTER(_VP), C.c_size_t]),
     "df_device_free": (C.c_int, [_VP]),
     "df_memcpy_h2d": (C.c_int, [_VP, _VP, C.c_size_t, _VP]),

@@ -14,9 +14,14 @@
 #include "df_kernels.h"
 #include "df_plan.h"
 
-namespace {
+#include "df_handle.h"
 
+namespace df {
+namespace api {
+
+namespace {
 thread_local std::string g_err;
+}
 
 int set_err(int code, const std::string& msg) {
     g_err = msg;
@@ -27,61 +32,14 @@ int hip_err(hipError_t e, const char* where) {
     return set_err(DF_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
 }
 
-struct DeviceGuard {
-    int prev = -1;
-    bool ok = false;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) == hipSuccess && (prev == dev || hipSetDevice(dev) == hipSuccess)) ok = true;
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
+const char* last_error() { return g_err.c_str(); }
 
-template <typename T>
-int upload(const std::vector<T>& v, void** dst) {
-    size_t bytes = v.size() * sizeof(T);
-    if (bytes == 0) bytes = 16;
-    hipError_t e = hipMalloc(dst, bytes);
-    if (e != hipSuccess) return set_err(DF_ERR_NOMEM, "hipMalloc failed for the chain plan");
-    if (!v.empty()) {
-        e = hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
-        if (e != hipSuccess) return hip_err(e, "hipMemcpy(plan)");
-    }
-    return DF_OK;
-}
+}  // namespace api
+}  // namespace df
 
-constexpr double kLog2Pi = 1.8378770664093453;  // log(2π)
+using namespace df::api;
 
-}  // namespace
-
-struct df_chain;
 static size_t lds_for_tiles(const df_chain* c, int t);
-
-struct df_chain {
-    df::Plan plan;
-    int device = 0;
-    void* d_layers = nullptr;
-    void* d_denses = nullptr;
-    void* d_chunks = nullptr;
-    void* d_stages = nullptr;
-    void* d_blob = nullptr;
-    void* d_tables = nullptr;
-    void* d_params = nullptr;
-    float* d_bounds = nullptr;  // [θmin (n) | θmax (n)]
-    bool has_bounds = false;
-    double* d_partial = nullptr;
-    int64_t partial_cap = 0;
-    int stage_bytes = 0;
-    int n_stage_bufs = 1;
-    void* d_sched = nullptr;    // [fwd schedule | bwd schedule]
-    void* d_ulayers = nullptr;  // specialised-kernel descriptors
-    int n_cu = 0;
-    int occ[4][df::kMaxTilesPerWave + 1] = {};  // resident workgroups per CU, by mode and tiles
-    int tab_bytes = 0;
-    size_t lds = 0;
-};
 
 static int uniform_variant(const df::Plan& P) { return P.uniform ? (P.relu_only ? 2 : 1) : 0; }
 
@@ -116,7 +74,7 @@ extern "C" {
 
 int df_get_abi_version(void) { return DF_ABI_VERSION; }
 
-const char* df_last_error(void) { return g_err.c_str(); }
+const char* df_last_error(void) { return last_error(); }
 
 int df_get_limits(df_limits* out) {
     if (!out) return set_err(DF_ERR_INVALID, "null pointer");
@@ -129,6 +87,7 @@ int df_get_limits(df_limits* out) {
 
 int df_chain_destroy(df_chain* c) {
     if (!c) return DF_OK;
+    if (c->n_trainers > 0) return set_err(DF_ERR_INVALID, "df_chain_destroy: destroy its df_train handles first");
     DeviceGuard gd(c->device);
     void* ptrs[] = {c->d_layers, c->d_denses, c->d_chunks, c->d_stages, c->d_blob,
                     c->d_tables, c->d_params, c->d_bounds, c->d_partial, c->d_sched, c->d_ulayers};
@@ -255,10 +214,11 @@ int df_chain_set_theta_bounds(df_chain* c, const float* tmin, const float* tmax)
 
 }  // extern "C"
 
-namespace {
+namespace df {
+namespace api {
 
-int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, float* xout, float* ldj,
-        float* lp, double* sum_out, int64_t batch, void* stream) {
+int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, float* xout, float* ldj, float* lp,
+        double* sum_out, int64_t batch, void* stream, float* snap) {
     if (!c) return set_err(DF_ERR_INVALID, "null chain");
     if (batch < 0) return set_err(DF_ERR_SHAPE, "negative batch size");
     const df::Plan& P = c->plan;
@@ -324,6 +284,7 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     a.n_sched_bwd = (int)P.sched_bwd.size();
     // Distributions.mvnormal_c0: -(d * log2π + logdetcov)/2 in Float32, logdet(I) = 0
     a.c0 = -((float)P.d * (float)kLog2Pi + 0.f) / 2.f;
+    a.snap = snap;
 
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipError_t e = df::launch_chain(P.ht, mode, P.outv != 0, uniform_variant(P), a, (unsigned)grid,
@@ -336,7 +297,8 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     return DF_OK;
 }
 
-}  // namespace
+}  // namespace api
+}  // namespace df
 
 extern "C" {
 

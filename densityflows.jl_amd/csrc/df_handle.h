@@ -1,0 +1,80 @@
+// df_handle.h — the df_chain handle and the host helpers shared by the C ABI
+// translation units (df_capi.hip: inference entry points, df_train_capi.hip:
+// training entry points).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "densityflows_hip.h"
+#include "df_kernels.h"
+#include "df_plan.h"
+
+struct df_chain {
+    df::Plan plan;
+    int device = 0;
+    void* d_layers = nullptr;
+    void* d_denses = nullptr;
+    void* d_chunks = nullptr;
+    void* d_stages = nullptr;
+    void* d_blob = nullptr;
+    void* d_tables = nullptr;
+    void* d_params = nullptr;
+    float* d_bounds = nullptr;  // [θmin (n) | θmax (n)]
+    bool has_bounds = false;
+    double* d_partial = nullptr;
+    int64_t partial_cap = 0;
+    int stage_bytes = 0;
+    int n_stage_bufs = 1;
+    void* d_sched = nullptr;    // [fwd schedule | bwd schedule]
+    void* d_ulayers = nullptr;  // specialised-kernel descriptors
+    int n_cu = 0;
+    int occ[4][df::kMaxTilesPerWave + 1] = {};  // resident workgroups per CU, by mode and tiles
+    int tab_bytes = 0;
+    size_t lds = 0;
+    int n_trainers = 0;         // live df_train handles bound to this chain
+};
+
+namespace df {
+namespace api {
+
+int set_err(int code, const std::string& msg);
+int hip_err(hipError_t e, const char* where);
+const char* last_error();
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) == hipSuccess && (prev == dev || hipSetDevice(dev) == hipSuccess)) ok = true;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+template <typename T>
+int upload(const std::vector<T>& v, void** dst) {
+    size_t bytes = v.size() * sizeof(T);
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(dst, bytes);
+    if (e != hipSuccess) return set_err(DF_ERR_NOMEM, "hipMalloc failed for the chain plan");
+    if (!v.empty()) {
+        e = hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_err(e, "hipMemcpy(plan)");
+    }
+    return DF_OK;
+}
+
+constexpr double kLog2Pi = 1.8378770664093453;  // log(2π)
+
+// Launch one fused chain pass.  flow: θ normalised with the handle's bounds;
+// snap (inverse modes, specialised kernel): every layer's output kept.
+int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, float* xout, float* ldj, float* lp,
+        double* sum_out, int64_t batch, void* stream, float* snap = nullptr);
+
+}  // namespace api
+}  // namespace df

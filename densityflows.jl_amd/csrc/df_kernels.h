@@ -43,6 +43,7 @@ struct ChainArgs {
     int n_sched_fwd;
     int n_sched_bwd;
     float c0;            // -(d·log2π)/2
+    float* snap;         // inverse modes, specialised kernel: state after each layer, [layer][sample][d]
 };
 
 // Per-variant entry points (explicitly instantiated in df_kernels_ht*.hip).

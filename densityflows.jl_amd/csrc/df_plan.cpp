@@ -307,6 +307,7 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                     DevDense DD{};
                     DD.in_kind = (k == 0) ? IN_STATE : IN_HIDDEN;
                     DD.n_out = D.out_dim;
+                    DD.in_dim = D.in_dim;
                     DD.act = D.act;
                     DD.has_bias = D.b ? 1 : 0;
                     DD.out_valu = (k + 1 == nd) && valu ? 1 : 0;
@@ -319,6 +320,13 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                     }
                     DD.mt = DD.out_valu ? 0 : (D.out_dim + 15) / 16;
                     prev_tiles = DD.mt;
+                    DD.w_off = (int32_t)P.trainables.size();
+                    for (int64_t q = 0; q < (int64_t)D.in_dim * D.out_dim; ++q) P.trainables.push_back(D.W[q]);
+                    DD.b_off = -1;
+                    if (D.b) {
+                        DD.b_off = (int32_t)P.trainables.size();
+                        for (int q = 0; q < D.out_dim; ++q) P.trainables.push_back(D.b[q]);
+                    }
                     int idx = (int)P.denses.size();
                     P.denses.push_back(DD);
                     if (DD.out_valu) {
@@ -369,11 +377,28 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                 DevDense& DD = P.denses[it.dense];
                 const df_dense_desc& D = src_of(it.dense);
                 const int out = D.out_dim, in = D.in_dim;
-                auto W = [&](int row, int k) -> float {
-                    return (row < out && k < in) ? D.W[(size_t)row + (size_t)out * k] : 0.f;
-                };
                 auto [st, off] = pk.alloc(it.bytes);
                 float* dst = pk.at(st, off);
+                const int64_t dst0 = (P.stages[st].src_off + off) / 4;  // blob float index of dst[0]
+                // W(row, k) at dst[q]: value, and the index map for device-side repacking
+                auto Wp = [&](float* at, int row, int k) {
+                    if (row < out && k < in) {
+                        *at = D.W[(size_t)row + (size_t)out * k];
+                        P.pack_dst.push_back((int32_t)(dst0 + (at - dst)));
+                        P.pack_src.push_back(DD.w_off + row + out * k);
+                    } else {
+                        *at = 0.f;
+                    }
+                };
+                auto Bp = [&](float* at, int row) {
+                    if (D.b && row < out) {
+                        *at = D.b[row];
+                        P.pack_dst.push_back((int32_t)(dst0 + (at - dst)));
+                        P.pack_src.push_back(DD.b_off + row);
+                    } else {
+                        *at = 0.f;
+                    }
+                };
                 if (it.kind == Item::CHUNK_KQ) {
                     // merge with the previous chunk of this dense when contiguous in the same stage
                     if (DD.n_chunks > 0) {
@@ -394,7 +419,7 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                         for (int m = 0; m < DD.mt; ++m)
                             for (int r = 0; r < DD.ks; ++r)
                                 for (int lane = 0; lane < 64; ++lane)
-                                    dst[(m * DD.ks + r) * 64 + lane] = W(16 * m + (lane & 15), 4 * r + (lane >> 4));
+                                    Wp(&dst[(m * DD.ks + r) * 64 + lane], 16 * m + (lane & 15), 4 * r + (lane >> 4));
                         continue;
                     }
                     // fragment [m][lane][r] for k-quad kq
@@ -407,20 +432,19 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                                 int k;
                                 if (DD.in_kind == IN_STATE) k = (s < DD.ks) ? 4 * s + g : in;  // beyond in → 0
                                 else k = 16 * it.kq + 4 * g + r;
-                                dst[(m * 64 + lane) * 4 + r] = W(row, k);
+                                Wp(&dst[(m * 64 + lane) * 4 + r], row, k);
                             }
                 } else if (it.kind == Item::BIAS) {
                     DD.bias_stage = st;
                     DD.bias_lds = off;
-                    for (int row = 0; row < DD.mt * 16; ++row)
-                        dst[row] = (D.b && row < out) ? D.b[row] : 0.f;
+                    for (int row = 0; row < DD.mt * 16; ++row) Bp(&dst[row], row);
                 } else {  // W3: VALU GEMV output  [o][16*kt_in] then b[4]
                     DD.w3_stage = st;
                     DD.w3_lds = off;
                     const int inp = 16 * DD.kt_in;
                     for (int o = 0; o < out; ++o)
-                        for (int k = 0; k < inp; ++k) dst[o * inp + k] = W(o, k);
-                    for (int o = 0; o < 4; ++o) dst[out * inp + o] = (D.b && o < out) ? D.b[o] : 0.f;
+                        for (int k = 0; k < inp; ++k) Wp(&dst[o * inp + k], o, k);
+                    for (int o = 0; o < 4; ++o) Bp(&dst[out * inp + o], o);
                 }
                 (void)in;
             }

@@ -58,7 +58,8 @@ struct DevDense {
     int32_t chunk0, n_chunks;
     int32_t w3_stage, w3_lds;      // VALU path: W [n_out][16*kt_in] row-major, then b[4]
     int32_t compact;               // IN_STATE, specialised kernel: [m][r < ks][lane] f32 (no k-quad padding)
-    int32_t pad1;
+    int32_t in_dim;                // true input width
+    int32_t w_off, b_off;          // offsets of weight / bias in the flat trainables vector (b_off -1: no bias)
 };
 
 struct DevLayer {
@@ -123,6 +124,11 @@ struct Plan {
     std::vector<int32_t> tables;
     std::vector<float> params;
     int64_t n_params = 0;
+    // Flux.trainables order (src/affine/RNVP.jl:51, NICE.jl:38, Blocks.jl:77): per
+    // coupling layer s_net then t_net, per Dense weight (out×in column-major) then bias.
+    std::vector<float> trainables;
+    // blob float index ← trainables index, for every blob float that holds a parameter
+    std::vector<int32_t> pack_dst, pack_src;
     double flops_per_sample = 0.0;
 };
 

@@ -1,0 +1,82 @@
+// df_train.h — launch interface of the training path (reverse sweep of the
+// NLL through the inverse pass, Adam, weight repacking).
+//
+// One training step (src/Flows.jl:396-414: Flux.gradient of
+// loss(backward(model, x, θ)) then Optimisers.update!):
+//   1. inverse pass on the specialised kernel, keeping every layer's output
+//      U[li] ([layer][sample][d], U[0] = z) and the Σ logpdf partials;
+//   2. z̄ = z / N (∂loss/∂z for loss = -mean(logpdf(MvNormal(0,I), z) + ldj));
+//   3. layers in chain order li = 0..L-1 (reverse of the inverse pass): one
+//      train_net_kernel launch per conditioner (s-net, then t-net), which
+//      recomputes the net on U[li+1], applies the coupling pullback
+//      (rrule(RNVP_backward) src/affine/RNVP.jl:119-143, NICE.jl:102-111),
+//      back-propagates through the Dense chain on MFMA, accumulates dW / db per
+//      workgroup in registers and updates z̄ in place; NormalizationLayer
+//      scales z̄ element-wise;
+//   4. a fixed-order reduction of the per-workgroup partials → ∇ (flat,
+//      Flux.trainables order); [multi-GPU: the caller all-reduces ∇ here];
+//   5. Adam (Optimisers.jl) on the flat parameters, then the packed weight
+//      blobs are regathered from them on device.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "df_plan.h"
+
+namespace df {
+
+constexpr int kTS = 20;  // row stride (floats) of the per-wave transpose buffers [row][16 samples]
+
+// One conditioner net of the specialised shape, as the training kernel sees it.
+struct GNet {
+    UNet u;                  // forward fragments (offsets rebased to the net's own LDS copy)
+    int32_t n_in;            // conditioner inputs (|axis_nn|)
+    int32_t h_true;          // hidden width
+    int32_t off_w0t;         // transposed region: W0ᵀ fragments [kq < HT][lane][4]
+    int32_t off_ht;          // transposed region: W_hᵀ fragments [kq][m][lane][4]
+    int32_t fwd_bytes;       // forward region bytes (16-B multiple)
+    int32_t t_bytes;         // transposed region bytes
+    int64_t fwd_src;         // byte offset of the forward region in the chain blob
+    int64_t t_src;           // byte offset of the transposed region in the training blob
+    int32_t p_begin, p_count;          // the net's contiguous slice of the trainables
+    int32_t w_off[3], b_off[3];        // first Dense, hidden Dense, output Dense (b_off -1: no bias)
+};
+
+enum : int { TR_PHASE_S = 0, TR_PHASE_T = 1 };
+
+struct TrainArgs {
+    const float* u_in;       // U[li+1]: the layer's input in the inverse pass
+    const float* u_out;      // U[li]:   its output
+    const float* theta;
+    const float* tmin;       // θ bounds (nullptr: θ used as given)
+    const float* tmax;
+    const int32_t* feat;     // [16] state slot of conditioner feature k (n + d → zero)
+    const int32_t* af;       // [n_af] state slots of the transformed dims
+    float* zbar;             // [sample][d] adjoint of the layer output, updated in place
+    float* ebuf;             // [sample][4] exp(-s) from the s-net launch
+    float* partial;          // [workgroup][p_total] gradient partials
+    const uint8_t* blob;     // chain weight blob (forward fragments)
+    const uint8_t* tblob;    // transposed fragments
+    int64_t batch;
+    int64_t p_total;
+    int d, n, n_af, kind, phase;
+    float inv_n;             // 1 / (global batch size)
+    GNet net;
+};
+
+size_t train_net_lds(int ht, const GNet& g);
+hipError_t set_train_lds_limit(size_t lds);
+hipError_t launch_train_net(int ht, int nh, bool relu, const TrainArgs& a, unsigned grid, size_t lds,
+                            hipStream_t st);
+hipError_t train_net_occupancy(int ht, int nh, bool relu, size_t lds, int* blocks);
+
+hipError_t launch_scale(float* dst, const float* src, float s, int64_t count, hipStream_t st);
+hipError_t launch_norm_adjoint(float* zbar, const float* xmin, const float* xmax, float alpha, float beta, int d,
+                               int64_t batch, hipStream_t st);
+hipError_t launch_reduce_grads(const float* partial, int n_parts, int64_t p_total, float* grad, hipStream_t st);
+hipError_t launch_adam(float* x, const float* g, float* m, float* v, int64_t count, float eta, float b1, float b2,
+                       float eps, float bt1, float bt2, hipStream_t st);
+hipError_t launch_repack(float* blob, const int32_t* dst, const int32_t* src, int64_t count, const float* params,
+                         hipStream_t st);
+
+}  // namespace df

@@ -1,0 +1,144 @@
+// df_train.hip — training kernels: the per-net reverse sweep (df_train_impl.h,
+// instantiated for hidden widths 16/32/64 and 0 or 1 hidden Dense), and the
+// element-wise steps around it (z̄ seed, NormalizationLayer adjoint, the
+// fixed-order gradient reduction, Adam, weight regathering).
+#include "df_train_impl.h"
+
+namespace df {
+
+namespace {
+
+void* train_ptr(int ht, int nh, bool relu) {
+#define DF_T(H)                                                                                   \
+    (nh ? (relu ? train_kernel_ptr<H, 1, true>() : train_kernel_ptr<H, 1, false>())               \
+        : (relu ? train_kernel_ptr<H, 0, true>() : train_kernel_ptr<H, 0, false>()))
+    switch (ht) {
+        case 1: return DF_T(1);
+        case 2: return DF_T(2);
+        case 4: return DF_T(4);
+        default: return nullptr;
+    }
+#undef DF_T
+}
+
+// z̄ = z / N
+__global__ void scale_kernel(float* dst, const float* src, float s, int64_t count) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) dst[i] = src[i] * s;
+}
+
+// NormalizationLayer inverse z = (β(x - x_min) + α(x_max - x)) / x_diff
+// (src/norm/Normalization.jl:66-76):  x̄ = z̄ · (β - α) / x_diff
+__global__ void norm_adjoint_kernel(float* zbar, const float* xmin, const float* xmax, float alpha, float beta,
+                                    int d, int64_t count) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) {
+        const int c = (int)(i % d);
+        zbar[i] = zbar[i] * ((beta - alpha) / (xmax[c] - xmin[c]));
+    }
+}
+
+// ∇[p] = Σ_w partial[w][p], w in increasing order (bitwise reproducible)
+__global__ void reduce_grads_kernel(const float* partial, int n_parts, int64_t p_total, float* grad) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= p_total) return;
+    float s = 0.f;
+    for (int w = 0; w < n_parts; ++w) s += partial[(int64_t)w * p_total + p];
+    grad[p] = s;
+}
+
+// Optimisers.Adam (apply!, Optimisers.jl v0.4):
+//   m = β1 m + (1-β1) g;  v = β2 v + (1-β2) g²
+//   x -= m / (1-β1ᵗ) / (sqrt(v / (1-β2ᵗ)) + ϵ) · η          (all Float32)
+__global__ void adam_kernel(float* x, const float* g, float* m, float* v, int64_t count, float eta, float b1,
+                            float b2, float eps, float bt1, float bt2) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const float gi = g[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * (gi * gi);
+    m[i] = mi;
+    v[i] = vi;
+    const float upd = mi / (1.f - bt1) / (sqrtf(vi / (1.f - bt2)) + eps) * eta;
+    x[i] = x[i] - upd;
+}
+
+__global__ void repack_kernel(float* blob, const int32_t* dst, const int32_t* src, int64_t count,
+                              const float* params) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) blob[dst[i]] = params[src[i]];
+}
+
+unsigned blocks_for(int64_t count, int threads) { return (unsigned)((count + threads - 1) / threads); }
+
+}  // namespace
+
+size_t train_net_lds(int ht, const GNet& g) {
+    const size_t tarea = (size_t)kWavesPerBlock * 2 * 16 * ht * kTS * 4;
+    const size_t red = (size_t)g.p_count * 4;
+    return (size_t)g.fwd_bytes + g.t_bytes + (tarea > red ? tarea : red);
+}
+
+hipError_t set_train_lds_limit(size_t lds) {
+    for (int ht : {1, 2, 4})
+        for (int nh = 0; nh < 2; ++nh)
+            for (int relu = 0; relu < 2; ++relu) {
+                hipError_t e = hipFuncSetAttribute(train_ptr(ht, nh, relu != 0),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                if (e != hipSuccess) return e;
+            }
+    return hipSuccess;
+}
+
+hipError_t launch_train_net(int ht, int nh, bool relu, const TrainArgs& a, unsigned grid, size_t lds,
+                            hipStream_t st) {
+    void* k = train_ptr(ht, nh, relu);
+    if (!k) return hipErrorInvalidValue;
+    void* args[] = {const_cast<TrainArgs*>(&a)};
+    return hipLaunchKernel(k, dim3(grid), dim3(kBlockThreads), args, lds, st);
+}
+
+hipError_t train_net_occupancy(int ht, int nh, bool relu, size_t lds, int* blocks) {
+    void* k = train_ptr(ht, nh, relu);
+    if (!k) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k, kBlockThreads, lds);
+}
+
+hipError_t launch_scale(float* dst, const float* src, float s, int64_t count, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(scale_kernel, dim3(blocks_for(count, 256)), dim3(256), 0, st, dst, src, s, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_norm_adjoint(float* zbar, const float* xmin, const float* xmax, float alpha, float beta, int d,
+                               int64_t batch, hipStream_t st) {
+    const int64_t count = batch * d;
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(norm_adjoint_kernel, dim3(blocks_for(count, 256)), dim3(256), 0, st, zbar, xmin, xmax,
+                       alpha, beta, d, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce_grads(const float* partial, int n_parts, int64_t p_total, float* grad, hipStream_t st) {
+    if (p_total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(reduce_grads_kernel, dim3(blocks_for(p_total, 256)), dim3(256), 0, st, partial, n_parts,
+                       p_total, grad);
+    return hipGetLastError();
+}
+
+hipError_t launch_adam(float* x, const float* g, float* m, float* v, int64_t count, float eta, float b1, float b2,
+                       float eps, float bt1, float bt2, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(count, 256)), dim3(256), 0, st, x, g, m, v, count, eta, b1, b2,
+                       eps, bt1, bt2);
+    return hipGetLastError();
+}
+
+hipError_t launch_repack(float* blob, const int32_t* dst, const int32_t* src, int64_t count, const float* params,
+                         hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(repack_kernel, dim3(blocks_for(count, 256)), dim3(256), 0, st, blob, dst, src, count, params);
+    return hipGetLastError();
+}
+
+}  // namespace df

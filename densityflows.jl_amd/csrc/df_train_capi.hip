@@ -1,0 +1,423 @@
+// df_train_capi.hip — the training entry points of the C ABI (df_train_*).
+//
+// Host side of one train! step (src/Flows.jl:396-414); the device work is in
+// df_train.hip / df_train_impl.h, the inverse pass with per-layer outputs in
+// the specialised chain kernel (df_uniform_impl.h, ChainArgs::snap).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+
+#include "df_handle.h"
+#include "df_train.h"
+
+using namespace df;
+using namespace df::api;
+
+namespace {
+
+struct SweepOp {
+    int layer;   // index in plan.layers
+    int net;     // index in df_train::nets, -1 for a NormalizationLayer
+    int phase;   // TR_PHASE_S / TR_PHASE_T
+};
+
+int round16(int v) { return (v + 15) / 16 * 16; }
+
+bool act_trainable(int a) {
+    return a == DF_ACT_IDENTITY || a == DF_ACT_RELU || a == DF_ACT_TANH || a == DF_ACT_SIGMOID;
+}
+
+}  // namespace
+
+struct df_train {
+    df_chain* c = nullptr;
+    df_adam opt{};
+    float bt1 = 0.f, bt2 = 0.f;  // βᵗ of the next update
+    int64_t P = 0;
+    int relu = 0;
+    std::vector<GNet> nets;
+    std::vector<int> net_nh;
+    std::vector<SweepOp> ops;
+    std::vector<uint8_t> tblob;
+    std::vector<int32_t> tdst, tsrc;
+    float* d_params = nullptr;
+    float* d_m = nullptr;
+    float* d_v = nullptr;
+    float* d_grad = nullptr;
+    float* d_partial = nullptr;
+    void* d_tblob = nullptr;
+    void* d_pdst = nullptr;
+    void* d_psrc = nullptr;
+    void* d_tdst = nullptr;
+    void* d_tsrc = nullptr;
+    float* d_snap = nullptr;
+    float* d_zbar = nullptr;
+    float* d_ebuf = nullptr;
+    double* d_lpsum = nullptr;
+    int64_t cap = 0;       // batch capacity of snap / zbar / ebuf
+    int grid = 0;          // workgroups of a full net launch (resident on the device)
+    size_t lds_max = 0;
+};
+
+namespace {
+
+void free_all(df_train* t) {
+    void* ptrs[] = {t->d_params, t->d_m, t->d_v,  t->d_grad, t->d_partial, t->d_tblob, t->d_pdst,
+                    t->d_psrc,   t->d_tdst, t->d_tsrc, t->d_snap, t->d_zbar,  t->d_ebuf,  t->d_lpsum};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+}
+
+// Transposed fragments of one net (W0ᵀ, W_hᵀ) appended to t->tblob with
+// their trainables index map.
+void pack_transposed(df_train* t, const Plan& P, GNet& g, const DevDense& D0, const DevDense* D1, int ht) {
+    const int h = g.h_true;
+    const size_t base = t->tblob.size();
+    g.t_src = (int64_t)base;
+    g.off_w0t = 0;
+    g.off_ht = ht * 1024;
+    const int bytes = ht * 1024 + (D1 ? ht * ht * 1024 : 0);
+    g.t_bytes = bytes;
+    t->tblob.resize(base + bytes, 0);
+    float* f = reinterpret_cast<float*>(t->tblob.data() + base);
+    const int64_t f0 = (int64_t)base / 4;
+    auto put = [&](int64_t q, int64_t src) {
+        f[q] = P.trainables[src];
+        t->tdst.push_back((int32_t)(f0 + q));
+        t->tsrc.push_back((int32_t)src);
+    };
+    // W0ᵀ: [kq][lane (i,g)][r] = W0[16kq + 4g + r, i]
+    for (int kq = 0; kq < ht; ++kq)
+        for (int lane = 0; lane < 64; ++lane)
+            for (int r = 0; r < 4; ++r) {
+                const int i = lane & 15, a = 16 * kq + 4 * (lane >> 4) + r;
+                if (a < h && i < g.n_in) put((int64_t)(kq * 64 + lane) * 4 + r, D0.w_off + a + (int64_t)h * i);
+            }
+    if (D1) {  // W1ᵀ: [kq][m][lane (i,g)][r] = W1[16kq + 4g + r, 16m + i]
+        const int64_t o = g.off_ht / 4;
+        for (int kq = 0; kq < ht; ++kq)
+            for (int m = 0; m < ht; ++m)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int r = 0; r < 4; ++r) {
+                        const int a = 16 * kq + 4 * (lane >> 4) + r, b = 16 * m + (lane & 15);
+                        if (a < h && b < h)
+                            put(o + ((int64_t)(kq * ht + m) * 64 + lane) * 4 + r, D1->w_off + a + (int64_t)h * b);
+                    }
+    }
+}
+
+int build_nets(df_train* t) {
+    const Plan& P = t->c->plan;
+    if (!P.uniform || !P.outv)
+        return set_err(DF_ERR_UNSUPPORTED,
+                       "training needs every conditioner in the default _dflt_net shape (hidden width <= 64) "
+                       "with <= 4 transformed dims per layer");
+    const int ht = P.ht;
+    for (int li = 0; li < P.n_layers; ++li) {
+        const DevLayer& L = P.layers[li];
+        if (L.kind == DF_LAYER_NORM) {
+            t->ops.push_back({li, -1, TR_PHASE_T});
+            continue;
+        }
+        const ULayer& U = P.ulayers[li];
+        auto add = [&](const UNet& u0, int d0, int nd, int phase) -> int {
+            if (u0.nh > 1) return set_err(DF_ERR_UNSUPPORTED, "training supports n_sublayers <= 2 (one hidden Dense)");
+            const DevDense& D0 = P.denses[d0];
+            const DevDense* D1 = u0.nh == 1 ? &P.denses[d0 + 1] : nullptr;
+            const DevDense& DO = P.denses[d0 + nd - 1];
+            for (int k = 0; k < nd; ++k)
+                if (!act_trainable(P.denses[d0 + k].act))
+                    return set_err(DF_ERR_UNSUPPORTED, "training supports σ ∈ {identity, relu, tanh, sigmoid}");
+            GNet g{};
+            g.u = u0;
+            g.n_in = D0.in_dim;
+            g.h_true = D0.n_out;
+            // the net's bytes inside its stage: [off_w0, end of the output GEMV block)
+            int lo = u0.off_w0;
+            lo = std::min(lo, u0.off_b0);
+            if (u0.nh) lo = std::min(lo, u0.off_h);
+            lo = std::min(lo, u0.off_out);
+            const int hi = u0.off_out + round16((u0.n_out * 16 * ht + 4) * 4);
+            g.fwd_src = P.stages[u0.stage].src_off + lo;
+            g.fwd_bytes = round16(hi - lo);
+            g.u.off_w0 -= lo;
+            g.u.off_b0 -= lo;
+            if (u0.nh) g.u.off_h -= lo;
+            g.u.off_out -= lo;
+            g.w_off[0] = D0.w_off;
+            g.b_off[0] = D0.b_off;
+            g.w_off[1] = D1 ? D1->w_off : D0.w_off;
+            g.b_off[1] = D1 ? D1->b_off : -1;
+            g.w_off[2] = DO.w_off;
+            g.b_off[2] = DO.b_off;
+            g.p_begin = D0.w_off;
+            int end = 0;
+            for (int k = 0; k < nd; ++k) {
+                const DevDense& D = P.denses[d0 + k];
+                end = std::max(end, D.w_off + D.in_dim * D.n_out);
+                if (D.b_off >= 0) end = std::max(end, D.b_off + D.n_out);
+            }
+            g.p_count = end - g.p_begin;
+            pack_transposed(t, P, g, D0, D1, ht);
+            t->nets.push_back(g);
+            t->net_nh.push_back(u0.nh);
+            t->ops.push_back({li, (int)t->nets.size() - 1, phase});
+            return DF_OK;
+        };
+        int rc = DF_OK;
+        if (L.kind == DF_LAYER_RNVP) rc = add(U.s, L.s_dense0, L.s_ndense, TR_PHASE_S);
+        if (rc == DF_OK) rc = add(U.t, L.t_dense0, L.t_ndense, TR_PHASE_T);
+        if (rc != DF_OK) return rc;
+    }
+    t->tblob.resize(t->tblob.size() + 16, 0);
+    return DF_OK;
+}
+
+int ensure_capacity(df_train* t, int64_t batch) {
+    if (batch <= t->cap) return DF_OK;
+    const Plan& P = t->c->plan;
+    for (float** p : {&t->d_snap, &t->d_zbar, &t->d_ebuf})
+        if (*p) {
+            (void)hipFree(*p);
+            *p = nullptr;
+        }
+    t->cap = 0;
+    const int64_t cap = std::max<int64_t>(batch, 1024);
+    if (hipMalloc(reinterpret_cast<void**>(&t->d_snap), sizeof(float) * P.n_layers * cap * P.d) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&t->d_zbar), sizeof(float) * cap * P.d) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&t->d_ebuf), sizeof(float) * cap * 4) != hipSuccess)
+        return set_err(DF_ERR_NOMEM, "hipMalloc failed (training activations)");
+    t->cap = cap;
+    return DF_OK;
+}
+
+int repack(df_train* t, hipStream_t st) {
+    df_chain* c = t->c;
+    const Plan& P = c->plan;
+    hipError_t e = launch_repack(static_cast<float*>(c->d_blob), static_cast<const int32_t*>(t->d_pdst),
+                                 static_cast<const int32_t*>(t->d_psrc), (int64_t)P.pack_dst.size(), t->d_params, st);
+    if (e == hipSuccess)
+        e = launch_repack(static_cast<float*>(t->d_tblob), static_cast<const int32_t*>(t->d_tdst),
+                          static_cast<const int32_t*>(t->d_tsrc), (int64_t)t->tdst.size(), t->d_params, st);
+    return e == hipSuccess ? DF_OK : hip_err(e, "repack kernel launch");
+}
+
+}  // namespace
+
+extern "C" {
+
+int df_train_destroy(df_train* t) {
+    if (!t) return DF_OK;
+    DeviceGuard gd(t->c->device);
+    free_all(t);
+    t->c->n_trainers--;
+    delete t;
+    return DF_OK;
+}
+
+int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
+    if (!out || !c) return set_err(DF_ERR_INVALID, "null pointer");
+    *out = nullptr;
+    df_train* t = new (std::nothrow) df_train();
+    if (!t) return set_err(DF_ERR_NOMEM, "host allocation failed");
+    t->c = c;
+    t->opt = opt ? *opt : df_adam{1e-3f, 0.9f, 0.999f, 1e-8f};
+    if (!(t->opt.eta >= 0.f) || !(t->opt.beta1 >= 0.f && t->opt.beta1 < 1.f) ||
+        !(t->opt.beta2 >= 0.f && t->opt.beta2 < 1.f) || !(t->opt.epsilon >= 0.f)) {
+        delete t;
+        return set_err(DF_ERR_INVALID, "invalid Adam hyper-parameters");
+    }
+    t->bt1 = t->opt.beta1;
+    t->bt2 = t->opt.beta2;
+    const Plan& P = c->plan;
+    t->P = (int64_t)P.trainables.size();
+    t->relu = P.relu_only;
+    int rc = build_nets(t);
+    if (rc != DF_OK) {
+        delete t;
+        return rc;
+    }
+    DeviceGuard gd(c->device);
+    if (!gd.ok) {
+        delete t;
+        return set_err(DF_ERR_HIP, "hipSetDevice failed");
+    }
+    c->n_trainers++;
+    // LDS and resident grid of the net kernels
+    for (size_t i = 0; i < t->nets.size(); ++i) t->lds_max = std::max(t->lds_max, train_net_lds(P.ht, t->nets[i]));
+    if (t->lds_max > 160 * 1024) {
+        df_train_destroy(t);
+        return set_err(DF_ERR_UNSUPPORTED, "training kernel needs more than 160 KiB of LDS");
+    }
+    hipError_t e = set_train_lds_limit(t->lds_max);
+    if (e != hipSuccess) {
+        df_train_destroy(t);
+        return hip_err(e, "hipFuncSetAttribute(train)");
+    }
+    int occ = 1;
+    for (size_t i = 0; i < t->nets.size(); ++i) {
+        int b = 1;
+        if (train_net_occupancy(P.ht, t->net_nh[i], t->relu != 0, t->lds_max, &b) == hipSuccess && b >= 1)
+            occ = (i == 0) ? b : std::min(occ, b);
+    }
+    t->grid = std::max(1, c->n_cu * occ);
+    const size_t pb = sizeof(float) * (size_t)std::max<int64_t>(t->P, 4);
+    if (hipMalloc(reinterpret_cast<void**>(&t->d_params), pb) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&t->d_m), pb) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&t->d_v), pb) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&t->d_grad), pb) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&t->d_partial), pb * t->grid) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&t->d_lpsum), sizeof(double)) != hipSuccess) {
+        df_train_destroy(t);
+        return set_err(DF_ERR_NOMEM, "hipMalloc failed (training state)");
+    }
+    if ((rc = upload(t->tblob, &t->d_tblob)) != DF_OK || (rc = upload(P.pack_dst, &t->d_pdst)) != DF_OK ||
+        (rc = upload(P.pack_src, &t->d_psrc)) != DF_OK || (rc = upload(t->tdst, &t->d_tdst)) != DF_OK ||
+        (rc = upload(t->tsrc, &t->d_tsrc)) != DF_OK) {
+        std::string m = last_error();
+        df_train_destroy(t);
+        return set_err(rc, m);
+    }
+    if (t->P > 0 && (hipMemcpy(t->d_params, P.trainables.data(), sizeof(float) * t->P, hipMemcpyHostToDevice) !=
+                         hipSuccess ||
+                     hipMemset(t->d_m, 0, sizeof(float) * t->P) != hipSuccess ||
+                     hipMemset(t->d_v, 0, sizeof(float) * t->P) != hipSuccess ||
+                     hipMemset(t->d_grad, 0, sizeof(float) * t->P) != hipSuccess)) {
+        df_train_destroy(t);
+        return set_err(DF_ERR_HIP, "initialising the training state failed");
+    }
+    *out = t;
+    return DF_OK;
+}
+
+int df_train_num_params(const df_train* t, int64_t* count) {
+    if (!t || !count) return set_err(DF_ERR_INVALID, "null pointer");
+    *count = t->P;
+    return DF_OK;
+}
+
+int df_train_grad_ptr(df_train* t, float** grad_dev) {
+    if (!t || !grad_dev) return set_err(DF_ERR_INVALID, "null pointer");
+    *grad_dev = t->d_grad;
+    return DF_OK;
+}
+
+int df_train_gradient(df_train* t, const float* x, const float* theta_raw, int64_t batch, int64_t n_total,
+                      double* logpdf_sum, void* stream) {
+    if (!t) return set_err(DF_ERR_INVALID, "null trainer");
+    if (batch < 0) return set_err(DF_ERR_SHAPE, "negative batch size");
+    if (n_total < batch || n_total < 1) return set_err(DF_ERR_INVALID, "n_total must be >= batch and >= 1");
+    df_chain* c = t->c;
+    const Plan& P = c->plan;
+    DeviceGuard gd(c->device);
+    if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (batch == 0) {
+        hipError_t e = hipMemsetAsync(t->d_grad, 0, sizeof(float) * t->P, st);
+        if (e == hipSuccess && logpdf_sum) e = hipMemsetAsync(logpdf_sum, 0, sizeof(double), st);
+        return e == hipSuccess ? DF_OK : hip_err(e, "hipMemsetAsync");
+    }
+    if (!x) return set_err(DF_ERR_INVALID, "null input array");
+    if (P.n > 0 && !theta_raw)
+        return set_err(DF_ERR_SHAPE, "dimensions θ must match (n, dims...) with n number of trained parameters");
+    int rc = ensure_capacity(t, batch);
+    if (rc != DF_OK) return rc;
+    const bool flow = c->has_bounds && P.n > 0;
+
+    // 1. inverse pass keeping every layer's output (U[li] = snap[li], U[0] = z)
+    rc = run(c, MODE_LOGPDF, flow, x, theta_raw, nullptr, nullptr, nullptr, logpdf_sum ? logpdf_sum : t->d_lpsum,
+             batch, stream, t->d_snap);
+    if (rc != DF_OK) return rc;
+    const int64_t bd = batch * P.d;
+    // 2. z̄ = z / N
+    const float inv_n = 1.f / (float)n_total;
+    hipError_t e = launch_scale(t->d_zbar, t->d_snap, inv_n, bd, st);
+    if (e != hipSuccess) return hip_err(e, "scale kernel launch");
+    // 3. reverse sweep, chain order
+    const int64_t ntiles = (batch + 15) / 16;
+    const int grid = (int)std::min<int64_t>(t->grid, (ntiles + kWavesPerBlock - 1) / kWavesPerBlock);
+    for (const SweepOp& op : t->ops) {
+        const DevLayer& L = P.layers[op.layer];
+        if (op.net < 0) {
+            const float* xmn = static_cast<const float*>(c->d_params) + L.norm_off;
+            e = launch_norm_adjoint(t->d_zbar, xmn, xmn + P.d, L.alpha, L.beta, P.d, batch, st);
+            if (e != hipSuccess) return hip_err(e, "norm adjoint launch");
+            continue;
+        }
+        TrainArgs a{};
+        a.u_in = (op.layer + 1 < P.n_layers) ? t->d_snap + (int64_t)(op.layer + 1) * bd : x;
+        a.u_out = t->d_snap + (int64_t)op.layer * bd;
+        a.theta = theta_raw;
+        a.tmin = flow ? c->d_bounds : nullptr;
+        a.tmax = flow ? c->d_bounds + P.n : nullptr;
+        a.feat = static_cast<const int32_t*>(c->d_tables) + L.feat_tab;
+        a.af = static_cast<const int32_t*>(c->d_tables) + L.af_tab;
+        a.zbar = t->d_zbar;
+        a.ebuf = t->d_ebuf;
+        a.partial = t->d_partial;
+        a.blob = static_cast<const uint8_t*>(c->d_blob);
+        a.tblob = static_cast<const uint8_t*>(t->d_tblob);
+        a.batch = batch;
+        a.p_total = t->P;
+        a.d = P.d;
+        a.n = P.n;
+        a.n_af = L.n_af;
+        a.kind = L.kind;
+        a.phase = op.phase;
+        a.inv_n = inv_n;
+        a.net = t->nets[op.net];
+        e = launch_train_net(P.ht, t->net_nh[op.net], t->relu != 0, a, (unsigned)grid, t->lds_max, st);
+        if (e != hipSuccess) return hip_err(e, "train kernel launch");
+    }
+    // 4. fixed-order reduction of the workgroup partials
+    e = launch_reduce_grads(t->d_partial, grid, t->P, t->d_grad, st);
+    return e == hipSuccess ? DF_OK : hip_err(e, "gradient reduction launch");
+}
+
+int df_train_apply(df_train* t, void* stream) {
+    if (!t) return set_err(DF_ERR_INVALID, "null trainer");
+    DeviceGuard gd(t->c->device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipError_t e = launch_adam(t->d_params, t->d_grad, t->d_m, t->d_v, t->P, t->opt.eta, t->opt.beta1,
+                               t->opt.beta2, t->opt.epsilon, t->bt1, t->bt2, st);
+    if (e != hipSuccess) return hip_err(e, "Adam kernel launch");
+    t->bt1 = t->bt1 * t->opt.beta1;  // βᵗ .* β in Float32
+    t->bt2 = t->bt2 * t->opt.beta2;
+    return repack(t, st);
+}
+
+int df_train_step(df_train* t, const float* x, const float* theta_raw, int64_t batch, double* logpdf_sum,
+                  void* stream) {
+    if (!t) return set_err(DF_ERR_INVALID, "null trainer");
+    if (batch == 0) return DF_OK;
+    int rc = df_train_gradient(t, x, theta_raw, batch, batch, logpdf_sum, stream);
+    return rc != DF_OK ? rc : df_train_apply(t, stream);
+}
+
+int df_train_get_params(df_train* t, float* host_out, int64_t count) {
+    if (!t || (!host_out && count > 0)) return set_err(DF_ERR_INVALID, "null pointer");
+    if (count != t->P) return set_err(DF_ERR_SHAPE, "count must equal df_train_num_params");
+    DeviceGuard gd(t->c->device);
+    if (count == 0) return DF_OK;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(host_out, t->d_params, sizeof(float) * count, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? DF_OK : hip_err(e, "hipMemcpy(params)");
+}
+
+int df_train_set_params(df_train* t, const float* host_in, int64_t count) {
+    if (!t || (!host_in && count > 0)) return set_err(DF_ERR_INVALID, "null pointer");
+    if (count != t->P) return set_err(DF_ERR_SHAPE, "count must equal df_train_num_params");
+    DeviceGuard gd(t->c->device);
+    if (count == 0) return DF_OK;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(t->d_params, host_in, sizeof(float) * count, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_err(e, "hipMemcpy(params)");
+    int rc = repack(t, nullptr);
+    if (rc != DF_OK) return rc;
+    e = hipDeviceSynchronize();
+    return e == hipSuccess ? DF_OK : hip_err(e, "repack");
+}
+
+}  // extern "C"

@@ -1,0 +1,342 @@
+// df_train_impl.h — the reverse-sweep kernel of one conditioner net.
+//
+// Every wave owns 16-sample tiles (persistent grid).  Per tile:
+//   forward recompute   x → A0 = σ0(W0 x + b0) [→ A1 = σh(W1 A0 + b1)] → y = σo(W3 h + b3)
+//                       (same device functions and rounding as the inverse
+//                       pass, so s and t are bitwise those of step 1);
+//   coupling pullback   s-net: s̄ = -z̄_af·z_af + 1/N (z_af = U[li]_af; j̄ = -1/N)
+//                       t-net: t̄ = -z̄_af·exp(-s)  (NICE: t̄ = -z̄_af),
+//                              then ū_af = z̄_af·exp(-s)   src/affine/RNVP.jl:133-139
+//   Dense backward      δ = ȳ ⊙ σ'(y);  dW += δ·inᵀ,  db += Σ δ;  in̄ = Wᵀ δ.
+// Wᵀδ chains on MFMA exactly like the forward pass (transposed fragments,
+// accumulator = next B operand).  dW = δ·inᵀ contracts over samples, which
+// sit on lanes 0..15 of the accumulator layout: both operands go through a
+// per-wave LDS transpose T[row][sample] and are read back as f32x4 fragments
+// (k-step s of lane group g uses sample 4g + s).  dW / db accumulate in
+// registers over all of a wave's tiles; the 8 waves are summed in LDS in a
+// fixed order and each workgroup writes its partial (no atomics: the final
+// reduction over workgroups is a separate fixed-order kernel, so gradients
+// are bitwise reproducible).
+// The conditioner input gradient is added to z̄ of the identity dims.
+#pragma once
+
+#include "df_train.h"
+#include "df_uniform_impl.h"
+
+namespace df {
+namespace trn {
+
+using impl::mfma4;
+
+__device__ __forceinline__ f32x4 lds4f(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// σ'(x) from y = σ(x) (ChainRules / NNlib derivative rules)
+__device__ __forceinline__ float act_grad(int act, float y) {
+    switch (act) {
+        case DF_ACT_RELU: return y > 0.f ? 1.f : 0.f;
+        case DF_ACT_TANH: return 1.f - y * y;
+        case DF_ACT_SIGMOID: return y * (1.f - y);
+        default: return 1.f;
+    }
+}
+
+template <int HT, bool RELU>
+__device__ __forceinline__ void mul_act_grad(int act, const f32x4 (&y)[HT], f32x4 (&gr)[HT]) {
+    if (RELU || act == DF_ACT_RELU) {
+#pragma unroll
+        for (int m = 0; m < HT; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gr[m][r] = (y[m][r] > 0.f) ? gr[m][r] : 0.f;
+    } else if (act != DF_ACT_IDENTITY) {
+#pragma unroll
+        for (int m = 0; m < HT; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gr[m][r] = gr[m][r] * act_grad(act, y[m][r]);
+    }
+}
+
+// accumulator-layout tile (rows 16m + 4g + r of sample j) → T[row][j]
+template <int HT>
+__device__ __forceinline__ void t_write(float* T, const f32x4 (&v)[HT]) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+#pragma unroll
+    for (int m = 0; m < HT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) T[(16 * m + 4 * g + r) * kTS + j] = v[m][r];
+}
+
+__device__ __forceinline__ float hsum4(f32x4 v) { return (v[0] + v[1]) + (v[2] + v[3]); }
+
+__device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+}  // namespace trn
+
+template <int HT, int NH, bool RELU>
+__global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a) {
+    using namespace trn;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const GNet& G = a.net;
+    const UNet& N = G.u;
+    uint8_t* fw = smem;
+    uint8_t* tw = smem + G.fwd_bytes;
+    float* tarea = reinterpret_cast<float*>(smem + G.fwd_bytes + G.t_bytes);
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, j = lane & 15;
+    const int d = a.d, n = a.n;
+    constexpr int TROWS = 16 * HT;
+    constexpr int INP = 16 * HT;
+    float* TA = tarea + wave * 2 * TROWS * kTS;
+    float* TB = TA + TROWS * kTS;
+    const bool sph = (a.phase == TR_PHASE_S);
+    const bool rnvp = (a.kind == DF_LAYER_RNVP);
+
+    {  // the net's forward and transposed fragments → LDS
+        const f32x4* src = reinterpret_cast<const f32x4*>(a.blob + G.fwd_src);
+        for (int i = tid; i < G.fwd_bytes / 16; i += kBlockThreads) reinterpret_cast<f32x4*>(fw)[i] = src[i];
+        const f32x4* srt = reinterpret_cast<const f32x4*>(a.tblob + G.t_src);
+        for (int i = tid; i < G.t_bytes / 16; i += kBlockThreads) reinterpret_cast<f32x4*>(tw)[i] = srt[i];
+    }
+    // zero rows of the δ_out transpose that no lane writes (rows >= 4)
+    for (int i = lane; i < TROWS * kTS; i += 64) TA[i] = 0.f;
+    __syncthreads();
+
+    constexpr int NHT = NH ? HT : 1;
+    f32x4 gW0[HT], gWo[HT], gWh[NHT][NHT];
+    float gb0[HT], gbh[NHT], gbo = 0.f;
+#pragma unroll
+    for (int m = 0; m < HT; ++m) {
+        gW0[m] = gWo[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        gb0[m] = 0.f;
+    }
+#pragma unroll
+    for (int m = 0; m < NHT; ++m) {
+        gbh[m] = 0.f;
+#pragma unroll
+        for (int q = 0; q < NHT; ++q) gWh[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    const int64_t ntiles = (a.batch + 15) / 16;
+    for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wave; tile < ntiles;
+         tile += (int64_t)gridDim.x * kWavesPerBlock) {
+        const int64_t s = tile * 16 + j;
+        const bool valid = s < a.batch;
+
+        // ---- conditioner input, features k = 4r + g of vcat(θ, u)[axis_nn] ----
+        float xin[1][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = 0.f;
+            if (r < N.ks && valid) {
+                const int slot = a.feat[4 * r + g];
+                if (slot < n) {
+                    v = a.theta[s * n + slot];
+                    if (a.tmin) {  // normalize_input (Data.jl:213-218)
+                        const float lo = a.tmin[slot], diff = a.tmax[slot] - lo;
+                        v = (diff == 0.f) ? 0.f : (v - lo) / diff;
+                    }
+                } else if (slot < n + d) {
+                    v = a.u_in[s * d + (slot - n)];
+                }
+            }
+            xin[0][r] = v;
+        }
+
+        // ---- forward recompute ----
+        f32x4 A0[1][HT], A1[1][HT];
+        uni::dense_first<HT, 1>(fw, N, xin, A0);
+        uni::bias_act<HT, 1, RELU>(fw + N.off_b0, N.act0, A0);
+        if constexpr (NH == 1) {
+            uni::dense_hidden<HT, 1>(fw + N.off_h, A0, A1);
+            uni::bias_act<HT, 1, RELU>(fw + N.off_h + HT * HT * 1024, N.acth, A1);
+        }
+        const f32x4(&H)[1][HT] = NH ? A1 : A0;
+        f32x4 o[1];
+        uni::out_valu<HT, 1, RELU>(fw, N, H, o);
+
+        // ---- coupling pullback → ȳ (every lane group holds all outputs of sample j) ----
+        float dout[4], zb[4], ee[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            dout[k] = 0.f;
+            zb[k] = 0.f;
+            ee[k] = 1.f;
+            if (k < a.n_af && valid) {
+                const int dim = a.af[k] - n;
+                zb[k] = a.zbar[s * d + dim];
+                if (sph) {
+                    ee[k] = expf(-o[0][k]);
+                    dout[k] = -zb[k] * a.u_out[s * d + dim] + a.inv_n;  // s̄ = -z̄_af·z_af - j̄
+                } else {
+                    if (rnvp) ee[k] = a.ebuf[s * 4 + k];
+                    dout[k] = -zb[k] * ee[k];                              // t̄ = -z̄_af·exp(-s)
+                }
+                if (!RELU && N.act_out != DF_ACT_IDENTITY) dout[k] = dout[k] * act_grad(N.act_out, o[0][k]);
+            }
+        }
+        if (sph && g == 0 && valid) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < a.n_af) a.ebuf[s * 4 + k] = ee[k];
+        }
+
+        // ---- output Dense: dW3 += ȳ·hᵀ, db3 += Σȳ, h̄ = W3ᵀ ȳ ----
+        if (g == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) TA[r * kTS + j] = dout[r];
+        }
+        t_write<HT>(TB, H[0]);
+        lds_order();
+        {
+            const f32x4 fa = lds4f(TA + j * kTS + 4 * g);
+            gbo += hsum4(fa);
+#pragma unroll
+            for (int mb = 0; mb < HT; ++mb) {
+                const f32x4 fb = lds4f(TB + (16 * mb + j) * kTS + 4 * g);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) gWo[mb] = mfma4(fa[q], fb[q], gWo[mb]);
+            }
+        }
+        f32x4 hb[1][HT];
+#pragma unroll
+        for (int m = 0; m < HT; ++m) hb[0][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < a.n_af) {
+#pragma unroll
+                for (int m = 0; m < HT; ++m) {
+                    const f32x4 w = impl::lds4(fw + N.off_out + ((k * INP + 16 * m + 4 * g) << 2));
+                    hb[0][m] = hb[0][m] + w * dout[k];
+                }
+            }
+        }
+        mul_act_grad<HT, RELU>(NH ? N.acth : N.act0, H[0], hb[0]);
+
+        // ---- hidden Dense: dW1 += δ·A0ᵀ, db1 += Σδ, Ā0 = W1ᵀ δ ----
+        f32x4 d0[1][HT];
+        if constexpr (NH == 1) {
+            lds_order();
+            t_write<HT>(TA, hb[0]);
+            t_write<HT>(TB, A0[0]);
+            lds_order();
+            f32x4 fa[HT], fb[HT];
+#pragma unroll
+            for (int m = 0; m < HT; ++m) {
+                fa[m] = lds4f(TA + (16 * m + j) * kTS + 4 * g);
+                fb[m] = lds4f(TB + (16 * m + j) * kTS + 4 * g);
+                gbh[m] += hsum4(fa[m]);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int ma = 0; ma < HT; ++ma)
+#pragma unroll
+                    for (int mb = 0; mb < HT; ++mb) gWh[ma][mb] = mfma4(fa[ma][q], fb[mb][q], gWh[ma][mb]);
+            uni::dense_hidden<HT, 1>(tw + G.off_ht, hb, d0);
+            mul_act_grad<HT, RELU>(N.act0, A0[0], d0[0]);
+        } else {
+#pragma unroll
+            for (int m = 0; m < HT; ++m) d0[0][m] = hb[0][m];
+        }
+
+        // ---- first Dense: dW0 += δ0·xᵀ, db0 += Σδ0, x̄ = W0ᵀ δ0 ----
+        lds_order();
+        t_write<HT>(TA, d0[0]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) TB[(4 * r + g) * kTS + j] = xin[0][r];
+        lds_order();
+        {
+            const f32x4 fb = lds4f(TB + j * kTS + 4 * g);
+#pragma unroll
+            for (int m = 0; m < HT; ++m) {
+                const f32x4 fa = lds4f(TA + (16 * m + j) * kTS + 4 * g);
+                gb0[m] += hsum4(fa);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) gW0[m] = mfma4(fa[q], fb[q], gW0[m]);
+            }
+        }
+        f32x4 xb = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kq = 0; kq < HT; ++kq) {
+            const f32x4 w = impl::lds4(tw + G.off_w0t + kq * 1024 + lane * 16);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xb = mfma4(w[r], d0[0][kq][r], xb);
+        }
+        if (valid) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int f = 4 * g + r;
+                if (f < G.n_in) {
+                    const int slot = a.feat[f];
+                    if (slot >= n && slot < n + d) a.zbar[s * d + (slot - n)] += xb[r];
+                }
+            }
+        }
+        if (!sph && rnvp && g == 0 && valid) {  // ū_af = z̄_af·exp(-s)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < a.n_af) a.zbar[s * d + (a.af[k] - n)] = zb[k] * ee[k];
+        }
+        lds_order();
+    }
+
+    // ---- workgroup reduction (fixed wave order) → partial[blockIdx.x] ----
+    __syncthreads();
+    float* R = tarea;
+    for (int i = tid; i < G.p_count; i += kBlockThreads) R[i] = 0.f;
+#pragma unroll
+    for (int m = 0; m < HT; ++m) gb0[m] = uni::xgroup_sum(gb0[m]);
+#pragma unroll
+    for (int m = 0; m < NHT; ++m) gbh[m] = uni::xgroup_sum(gbh[m]);
+    gbo = uni::xgroup_sum(gbo);
+    __syncthreads();
+    const int h = G.h_true;
+    const int wo0 = G.w_off[0] - G.p_begin, bo0 = G.b_off[0] - G.p_begin;
+    const int wo1 = G.w_off[1] - G.p_begin, bo1 = G.b_off[1] - G.p_begin;
+    const int wo2 = G.w_off[2] - G.p_begin, bo2 = G.b_off[2] - G.p_begin;
+    for (int w = 0; w < kWavesPerBlock; ++w) {
+        if (wave == w) {
+#pragma unroll
+            for (int m = 0; m < HT; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 16 * m + 4 * g + r;
+                    if (row < h && j < G.n_in) R[wo0 + row + h * j] += gW0[m][r];
+                    const int ob = 16 * m + j;  // output Dense: row o = 4g + r, column ob
+                    if (4 * g + r < N.n_out && ob < h) R[wo2 + (4 * g + r) + N.n_out * ob] += gWo[m][r];
+                }
+            if (g == 0) {
+#pragma unroll
+                for (int m = 0; m < HT; ++m)
+                    if (G.b_off[0] >= 0 && 16 * m + j < h) R[bo0 + 16 * m + j] += gb0[m];
+                if (G.b_off[2] >= 0 && j < N.n_out) R[bo2 + j] += gbo;
+            }
+            if constexpr (NH == 1) {
+#pragma unroll
+                for (int ma = 0; ma < HT; ++ma)
+#pragma unroll
+                    for (int mb = 0; mb < HT; ++mb)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int row = 16 * ma + 4 * g + r, col = 16 * mb + j;
+                            if (row < h && col < h) R[wo1 + row + h * col] += gWh[ma][mb][r];
+                        }
+                if (g == 0) {
+#pragma unroll
+                    for (int m = 0; m < HT; ++m)
+                        if (G.b_off[1] >= 0 && 16 * m + j < h) R[bo1 + 16 * m + j] += gbh[m];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    float* dst = a.partial + (int64_t)blockIdx.x * a.p_total + G.p_begin;
+    for (int i = tid; i < G.p_count; i += kBlockThreads) dst[i] = R[i];
+}
+
+template <int HT, int NH, bool RELU>
+void* train_kernel_ptr() {
+    return reinterpret_cast<void*>(&train_net_kernel<HT, NH, RELU>);
+}
+
+}  // namespace df

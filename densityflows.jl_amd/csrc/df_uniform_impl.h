@@ -437,6 +437,14 @@ uniform_kernel(ChainArgs a) {
             }
         }
         have_acc = have_acc || last_in_elem;
+        if (!FWD && a.snap) {  // training: keep every layer's output for the reverse sweep
+            float* dst = a.snap + (int64_t)li * a.batch * d;
+            for (int tt = 0; tt < nt; ++tt) {
+                const int smp = (wave * nt + tt) * 16 + j;
+                if (smp < nvalid)
+                    for (int i = g; i < d; i += 4) dst[(s0 + smp) * d + i] = state[row0 + tt * tstep + n + i];
+            }
+        }
     }
 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -183,6 +183,60 @@ int df_flow_logpdf(df_chain* chain, const float* x, const float* theta_raw,
 int df_flow_logpdf_sum(df_chain* chain, const float* x, const float* theta_raw,
                        double* sum_out, int64_t batch, void* stream);
 
+/* ---- training ---------------------------------------------------------------
+ * train!(flow, data, opt_state; ...) src/Flows.jl:380-445: per batch
+ *   grads = Flux.gradient(m -> loss(backward(m, x, θ)...), flow.model)   (:398-411)
+ *   Optimisers.update!(opt_state, flow.model, grads[1])                  (:413)
+ * with loss = -mean(logpdf(MvNormal(0, I), z) .+ ldj)  (src/Flows.jl:352-359)
+ * and the custom pullbacks rrule(RNVP_backward) (src/affine/RNVP.jl:99-147),
+ * rrule(NICE_backward) (src/affine/NICE.jl:84-113).
+ *
+ * A df_train handle owns the flat trainable parameters of its chain in
+ * Flux.trainables order (per coupling layer: s_net then t_net; per Dense:
+ * weight (out×in column-major) then bias; NormalizationLayer: none), the
+ * Adam state and the gradient buffer, and rewrites the chain's packed
+ * weights after every update, so df_chain_* / df_flow_* calls on the chain
+ * see the trained parameters.  Supported: chains whose conditioners all have
+ * the default _dflt_net shape (src/Layers.jl:33-50) with n_sublayers 1 or 2,
+ * hidden width <= 64, <= 4 transformed dims per layer and σ in {identity,
+ * relu, tanh, sigmoid}; other chains return DF_ERR_UNSUPPORTED. */
+
+typedef struct df_train df_train;
+
+/* Optimisers.Adam(η, β, ϵ) (Optimisers.jl v0.4; defaults 1e-3, (0.9, 0.999), 1e-8) */
+typedef struct df_adam {
+    float eta;
+    float beta1, beta2;
+    float epsilon;
+} df_adam;
+
+/* Optimisers.setup(Adam(...), flow.model): state m = v = 0, βᵗ = β. */
+int df_train_create(df_train** out, df_chain* chain, const df_adam* opt);
+int df_train_destroy(df_train* t);
+/* Number of trainable parameters (length of the flat vectors below). */
+int df_train_num_params(const df_train* t, int64_t* count);
+/* Gradient of loss over this batch with the mean taken over `n_total`
+ * samples (n_total = batch on one GPU; the global batch under data
+ * parallelism, so the per-rank gradients SUM to the global one).  θ is
+ * normalised with the chain's bounds when set (df_chain_set_theta_bounds),
+ * as train! does with normalized_training_data (src/Data.jl:189-193).
+ * The result is left in the device buffer returned by df_train_grad_ptr.
+ * `logpdf_sum` (device double, may be NULL) receives Σ logpdf of the batch
+ * at the current parameters (the loss before the update is -Σ/n_total). */
+int df_train_gradient(df_train* t, const float* x, const float* theta_raw, int64_t batch, int64_t n_total,
+                      double* logpdf_sum, void* stream);
+/* Device pointer of the flat gradient (count floats); all-reduce it here
+ * for multi-GPU data parallelism. */
+int df_train_grad_ptr(df_train* t, float** grad_dev);
+/* One Adam step with the current gradient; repacks the chain's weights. */
+int df_train_apply(df_train* t, void* stream);
+/* df_train_gradient (n_total = batch) followed by df_train_apply. */
+int df_train_step(df_train* t, const float* x, const float* theta_raw, int64_t batch, double* logpdf_sum,
+                  void* stream);
+/* Copy the current trainables to / from host memory (count floats). */
+int df_train_get_params(df_train* t, float* host_out, int64_t count);
+int df_train_set_params(df_train* t, const float* host_in, int64_t count);
+
 /* ---- device memory helpers (for hosts without a GPU array package) ------ */
 int df_device_alloc(void** ptr, size_t bytes);
 int df_device_free(void* ptr);

@@ -483,3 +483,156 @@ def coupling_block(rng, first_axes, **kw):
 
 def num_params(net):
     return sum(l["W"].size + (0 if l.get("b") is None else l["b"].size) for l in net)
+
+
+# ----------------------------------------------------------------------------
+# Training: gradient of the NLL through the inverse pass, Adam
+# (src/Flows.jl:380-445, custom pullback src/affine/RNVP.jl:99-147)
+# ----------------------------------------------------------------------------
+
+_ACT_GRAD = {
+    # derivative of σ expressed through the output y = σ(x) (and x where needed)
+    "identity": lambda x, y: np.ones_like(y),
+    "relu": lambda x, y: (x > 0).astype(y.dtype),
+    "tanh": lambda x, y: 1 - y * y,
+    "sigmoid": lambda x, y: y * (1 - y),
+}
+
+
+def _mlp_forward_cache(net, x, dtype):
+    """Forward through a conditioner keeping (pre, post) activations per Dense."""
+    cache = []
+    h = x
+    for layer in net:
+        W = np.asarray(layer["W"], dtype=dtype)
+        pre = W @ h
+        if layer.get("b") is not None:
+            pre = pre + np.asarray(layer["b"], dtype=dtype)[:, None]
+        post = activation(layer["act"], pre)
+        cache.append((h, pre, post))
+        h = post
+    return h, cache
+
+
+def _mlp_backward(net, cache, gout, dtype):
+    """Reverse-mode through the Dense chain (Flux/Zygote semantics):
+    returns (d input, [(dW, db), ...])."""
+    grads = [None] * len(net)
+    g = gout
+    for k in range(len(net) - 1, -1, -1):
+        layer = net[k]
+        h, pre, post = cache[k]
+        if layer["act"] not in _ACT_GRAD:
+            raise NotImplementedError(f"gradient of {layer['act']}")
+        d = g * _ACT_GRAD[layer["act"]](pre, post)
+        dW = d @ h.T
+        db = d.sum(axis=1) if layer.get("b") is not None else None
+        grads[k] = (dW, db)
+        g = np.asarray(layer["W"], dtype=dtype).T @ d
+    return g, grads
+
+
+def _flat_layers(elem):
+    k = elem["kind"]
+    if k == "chain":
+        out = []
+        for e in elem["layers"]:
+            out += _flat_layers(e)
+        return out
+    if k == "block":
+        return [elem["layer_1"], elem["layer_2"]]
+    return [elem]
+
+
+def nll_and_grad(chain, x, theta, n_total=None, dtype=np.float64):
+    """loss = -mean(logpdf(base, z) .+ ldj) with (z, ldj) = backward(chain, x, θ)
+    (src/Flows.jl:352-359, :400-413) and its gradient w.r.t. every Dense weight
+    and bias.  The mean is over ``n_total`` samples (default: x.shape[1]) so that
+    shard gradients sum to the global one.  Returns (loss_sum_part, grads) where
+    grads mirrors the flattened layer list: for each coupling layer a dict
+    {"s_net": [(dW, db), ...], "t_net": [...]} (None for NormalizationLayer)."""
+    layers = _flat_layers(chain)
+    B = x.shape[1]
+    N = float(n_total if n_total is not None else B)
+    u = np.asarray(x, dtype=dtype)
+    th = np.asarray(theta, dtype=dtype).reshape(-1, B)
+    saved = []
+    ldj = np.zeros(B, dtype=dtype)
+    # inverse pass, last layer first (src/Chains.jl:149-165)
+    for L in reversed(layers):
+        k = L["kind"]
+        if k == "norm":
+            saved.append((L, u, None))
+            u, l = norm_backward(L, u, th, dtype)
+            ldj = ldj + l
+            continue
+        inp = _conditioner_input(L, u, th, dtype)
+        t, tcache = _mlp_forward_cache(L["t_net"], inp, dtype)
+        if k == "rnvp":
+            s, scache = _mlp_forward_cache(L["s_net"], inp, dtype)
+        else:
+            s, scache = np.zeros_like(t), None
+        af = np.asarray(L["axis_af"], dtype=np.int64) - 1
+        z = u.copy()
+        z[af, :] = (u[af, :] - t) * np.exp(-s)
+        saved.append((L, u, (inp, s, t, scache, tcache, af, z)))
+        if k == "rnvp":
+            ldj = ldj - _ldj_sum(s)
+        u = z
+    z = u
+    lp = mvnormal_logpdf(z, dtype) + ldj
+    loss_part = -np.sum(lp) / N
+    # reverse mode: d loss / d z = z / N ; d loss / d ldj = -1/N
+    zbar = z / N
+    jbar = -1.0 / N
+    grads = []
+    for L, u_in, extra in reversed(saved):
+        if L["kind"] == "norm":
+            xmin = np.asarray(L["x_min"], dtype=dtype)[:, None]
+            xmax = np.asarray(L["x_max"], dtype=dtype)[:, None]
+            zbar = zbar * (dtype(L["beta"]) - dtype(L["alpha"])) / (xmax - xmin)
+            grads.append(None)
+            continue
+        inp, s, t, scache, tcache, af, z = extra
+        e = np.exp(-s)
+        zbar_af = zbar[af, :]
+        # rrule(RNVP_backward), src/affine/RNVP.jl:119-143
+        sbar = -zbar_af * (u_in[af, :] - t) * e - jbar
+        tbar = -zbar_af * e
+        ubar = zbar.copy()
+        ubar[af, :] = zbar_af * e
+        g_in_t, gt = _mlp_backward(L["t_net"], tcache, tbar, dtype)
+        g_in = g_in_t
+        gs = None
+        if L["kind"] == "rnvp":
+            g_in_s, gs = _mlp_backward(L["s_net"], scache, sbar, dtype)
+            g_in = g_in + g_in_s
+        else:
+            # NICE_backward pullback (src/affine/NICE.jl:102-111): t̄ = -z̄_af, ū = z̄
+            pass
+        # scatter the conditioner-input gradient back to the state rows
+        # (vcat(θ, u)[axis_nn]; θ gets no gradient that we keep)
+        nn = np.asarray(L["axis_nn"], dtype=np.int64) - 1
+        n = L["n"]
+        for kk, slot in enumerate(nn):
+            if slot >= n:
+                ubar[slot - n, :] += g_in[kk, :]
+        zbar = ubar
+        grads.append({"s_net": gs, "t_net": gt})
+    # reversed(saved) visits layers in chain order, so grads already is
+    return loss_part, grads
+
+
+def adam_update(params, grads, state, eta=1e-3, beta=(0.9, 0.999), eps=1e-8):
+    """Optimisers.Adam (v0.4) on flat float arrays, in place:
+    m = β1 m + (1-β1) g;  v = β2 v + (1-β2) g²;
+    x -= η · (m / (1-β1^t)) / (sqrt(v / (1-β2^t)) + ϵ)."""
+    T = params.dtype.type  # Optimisers: η, β, ϵ converted to the parameter eltype
+    eta, beta, eps = T(eta), (T(beta[0]), T(beta[1])), T(eps)
+    m, v, bt = state
+    m[:] = beta[0] * m + (1 - beta[0]) * grads
+    v[:] = beta[1] * v + (1 - beta[1]) * (grads * grads)  # (1 - β2) * abs2(dx)
+    upd = m / (1 - bt[0]) / (np.sqrt(v / (1 - bt[1])) + eps) * eta
+    params -= upd
+    state[2] = (bt[0] * beta[0], bt[1] * beta[1])
+    return params

@@ -1,0 +1,288 @@
+"""GPU parity of the training path (df_train_* through the C ABI) against the
+oracle's reverse-mode restatement (oracle/flow_oracle.py: nll_and_grad,
+adam_update — pinned by finite differences in tests/test_oracle.py).
+
+Criteria:
+  * gradient: fp32 device sums vs the fp64 oracle, per Dense tensor,
+    |g - g_ref| <= 1e-4·|g_ref| + 2e-5·max|g_ref| (reductions over the batch
+    reorder fp32 sums; the same criterion as helpers.close, looser rtol);
+  * Adam: the device update equals the Float32 formula evaluated in numpy
+    from the same gradient to 1 ulp;
+  * reproducibility: two gradient evaluations are bitwise identical (fixed
+    reduction order, no atomics).
+"""
+import numpy as np
+import pytest
+
+import densityflows_amd as dfa
+from densityflows_amd.train import Adam, HIPTrainer, load_trainables, setup, train_, trainables
+from helpers import close, spec_to_element
+from oracle import flow_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+G_RTOL = 1e-4
+G_ATOL = 2e-5
+
+
+def _dev(a, dev):
+    """numpy (rows, B) → flat Julia-order device buffer."""
+    import torch
+
+    a = np.asarray(a, np.float32)
+    return torch.from_numpy(np.ascontiguousarray(a.T).ravel()).to(dev)
+
+
+def _flat_oracle_grads(spec, grads):
+    parts = []
+    for L, g in zip(O._flat_layers(spec), grads):
+        if L["kind"] == "norm":
+            continue
+        for net in ("s_net", "t_net"):
+            if net not in L:
+                continue
+            for (dW, db), D in zip(g[net], L[net]):
+                parts.append(np.asarray(dW).ravel(order="F"))
+                if D.get("b") is not None:
+                    parts.append(np.asarray(db))
+    return np.concatenate(parts)
+
+
+def _tensor_slices(spec):
+    out, o = [], 0
+    for L in O._flat_layers(spec):
+        if L["kind"] == "norm":
+            continue
+        for net in ("s_net", "t_net"):
+            for D in L.get(net, []):
+                out.append(slice(o, o + D["W"].size))
+                o += D["W"].size
+                if D.get("b") is not None:
+                    out.append(slice(o, o + D["b"].size))
+                    o += D["b"].size
+    return out
+
+
+def _readme_spec(rng, hidden=16):
+    """test/runtests.jl:103-109: three RNVP layers + NormalizationLayer(x, -1, 1)."""
+    layers = [O.rnvp_layer(rng, O.coupling_axes(5, m, n=1), hidden=hidden, bias_scale=0.1, out_scale=0.5)
+              for m in ([1, 2, 3], [3, 4, 5], [5, 1, 2])]
+    layers.append({"kind": "norm", "x_min": np.full(5, -3.0, np.float32), "x_max": np.full(5, 2.5, np.float32),
+                   "alpha": -1.0, "beta": 1.0})
+    return {"kind": "chain", "layers": layers}
+
+
+def _cfg2_spec(rng):
+    """BASELINE configs[1]: FlowChain(CouplingBlock, 4, 5; hidden 64), n = 0."""
+    blocks = []
+    for _ in range(4):
+        blocks.append(O.coupling_block(rng, O.coupling_axes_cut(5, n=0), hidden=64, bias_scale=0.1,
+                                       out_scale=0.1))
+    return {"kind": "chain", "layers": blocks}
+
+
+def _mixed_spec(rng):
+    """tanh / sigmoid conditioners, n_sublayers = 1, a NICE layer, hidden 32."""
+    nice = O.rnvp_layer(rng, O.coupling_axes(6, [2, 5], n=2), hidden=32, act="tanh", bias_scale=0.1)
+    nice["kind"] = "nice"
+    del nice["s_net"]
+    return {"kind": "chain", "layers": [
+        O.rnvp_layer(rng, O.coupling_axes(6, [1, 3, 6], n=2), hidden=32, act="tanh", bias_scale=0.1,
+                     out_scale=0.5),
+        nice,
+        O.coupling_block(rng, O.coupling_axes_cut(6, 2, n=2), n_sub=1, hidden=32, act="sigmoid",
+                         bias_scale=0.1, out_scale=0.5),
+    ]}
+
+
+SPECS = {"readme": (_readme_spec, 5, 1), "cfg2": (_cfg2_spec, 5, 0), "mixed": (_mixed_spec, 6, 2)}
+
+
+def _setup(name, seed=0):
+    make, d, n = SPECS[name]
+    rng = np.random.default_rng(seed)
+    spec = make(rng)
+    chain = spec_to_element(spec)
+    return spec, chain, d, n
+
+
+def _inputs(d, n, B, seed=1):
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((d, B)).astype(np.float32)
+    th = rng.random((n, B)).astype(np.float32) if n > 0 else np.zeros((0, B), np.float32)
+    return x, th
+
+
+def _gpu_grad(tr, x, th, cuda, n_total=None):
+    import torch
+
+    B = x.shape[1]
+    lp = torch.zeros(1, dtype=torch.float64, device=cuda)
+    tr.gradient(_dev(x, cuda), _dev(th, cuda) if th.shape[0] else None, B, n_total or B, lp)
+    torch.cuda.synchronize()
+    return tr.grad().detach().cpu().numpy().copy(), float(lp.item())
+
+
+@pytest.mark.parametrize("name,B", [("readme", 1000), ("cfg2", 3001), ("mixed", 777), ("readme", 1), ("cfg2", 17)])
+def test_gradient_parity(cuda, name, B):
+    spec, chain, d, n = _setup(name)
+    tr = HIPTrainer(chain.hip(), Adam())
+    np.testing.assert_array_equal(tr.get_params(), trainables(chain))
+    x, th = _inputs(d, n, B)
+    g, lpsum = _gpu_grad(tr, x, th, cuda)
+    loss, ref = O.nll_and_grad(spec, x, th if n else np.zeros((0, B)))
+    ref = _flat_oracle_grads(spec, ref)
+    assert g.shape == ref.shape
+    assert abs(-lpsum / B - loss) <= 1e-5 * max(1.0, abs(loss))
+    worst = 0.0
+    for sl in _tensor_slices(spec):
+        ok, r = close(g[sl], ref[sl], G_RTOL, G_ATOL)
+        worst = max(worst, r)
+    assert worst <= 1.0, f"gradient violation ratio {worst}"
+
+
+def test_gradient_bitwise_reproducible(cuda):
+    spec, chain, d, n = _setup("cfg2")
+    tr = HIPTrainer(chain.hip(), Adam())
+    x, th = _inputs(d, n, 20000)
+    g1, _ = _gpu_grad(tr, x, th, cuda)
+    g2, _ = _gpu_grad(tr, x, th, cuda)
+    np.testing.assert_array_equal(g1, g2)
+
+
+def test_gradient_shards_sum(cuda):
+    """Data-parallel contract: shard gradients with n_total = global batch sum to the full gradient."""
+    spec, chain, d, n = _setup("readme")
+    tr = HIPTrainer(chain.hip(), Adam())
+    x, th = _inputs(d, n, 2000)
+    g, _ = _gpu_grad(tr, x, th, cuda)
+    ga, _ = _gpu_grad(tr, x[:, :700], th[:, :700], cuda, n_total=2000)
+    gb, _ = _gpu_grad(tr, x[:, 700:], th[:, 700:], cuda, n_total=2000)
+    for sl in _tensor_slices(spec):
+        assert close(ga[sl] + gb[sl], g[sl], 1e-5, 1e-6)[0]
+
+
+def test_empty_batch_gradient_is_zero(cuda):
+    spec, chain, d, n = _setup("readme")
+    tr = HIPTrainer(chain.hip(), Adam())
+    x, th = _inputs(d, n, 100)
+    _gpu_grad(tr, x, th, cuda)
+    import torch
+
+    tr.gradient(None, None, 0, 1, None)
+    torch.cuda.synchronize()
+    assert not np.any(tr.grad().cpu().numpy())
+
+
+def _ulp_diff(a, b):
+    ai = np.asarray(a, np.float32).view(np.int32).astype(np.int64)
+    bi = np.asarray(b, np.float32).view(np.int32).astype(np.int64)
+    return int(np.max(np.abs(ai - bi))) if ai.size else 0
+
+
+@pytest.mark.parametrize("name", ["readme", "mixed"])
+def test_adam_step_and_repack(cuda, name):
+    """Optimisers.update! on the device: the Float32 Adam formula to 1 ulp over
+    two steps (βᵗ advances), and the chain's packed weights follow the update
+    (forward / backward use the new parameters)."""
+    spec, chain, d, n = _setup(name)
+    opt = Adam(2e-3, (0.8, 0.99), 1e-7)
+    tr = HIPTrainer(chain.hip(), opt)
+    p = tr.get_params().copy()
+    st = [np.zeros_like(p), np.zeros_like(p), (np.float32(0.8), np.float32(0.99))]
+    for step in range(2):
+        x, th = _inputs(d, n, 512, seed=10 + step)
+        g, _ = _gpu_grad(tr, x, th, cuda)
+        p = tr.get_params().copy()
+        tr.apply()
+        O.adam_update(p, g, st, eta=np.float32(2e-3), beta=(np.float32(0.8), np.float32(0.99)),
+                      eps=np.float32(1e-7))
+        assert _ulp_diff(tr.get_params(), p) <= 1
+    # the chain now evaluates the updated parameters
+    load_trainables(chain, tr.get_params())
+    x, th = _inputs(d, n, 300, seed=99)
+    z, l = dfa.backward(chain, x, th if n else None)
+    zo, lo = O.backward(chain.to_spec(), x, th if n else np.zeros((0, 300)))
+    assert close(z, zo)[0] and close(l, lo)[0]
+
+
+def test_set_params_roundtrip(cuda):
+    spec, chain, d, n = _setup("readme")
+    tr = HIPTrainer(chain.hip(), Adam())
+    p = tr.get_params()
+    q = (p * np.float32(0.5)).astype(np.float32)
+    tr.set_params(q)
+    np.testing.assert_array_equal(tr.get_params(), q)
+    load_trainables(chain, q)
+    x, th = _inputs(d, n, 64, seed=3)
+    xf, lf = dfa.forward(chain, x, th)
+    xo, lo = O.forward(chain.to_spec(), x, th)
+    assert close(xf, xo)[0] and close(lf, lo)[0]
+
+
+def test_train_runtests_flow(cuda):
+    """test/runtests.jl:97-121: datatest.jld2 fixture, README chain, Adam(1f-3),
+    train!(epochs = 5), then sample(flow, (2, 5, 7), (-1f0,))."""
+    import os
+
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    x = np.load(os.path.join(here, "datatest_x.npy"))
+    th = np.load(os.path.join(here, "datatest_theta.npy"))
+    rng = np.random.default_rng(0)
+    data = dfa.DataArrays(x, th, rng=rng)
+    chain = dfa.FlowChain(
+        dfa.CouplingLayer(data, [1, 2, 3], hidden_dim_s=16, hidden_dim_t=16, rng=rng),
+        dfa.CouplingLayer(data, [3, 4, 5], hidden_dim_s=16, hidden_dim_t=16, rng=rng),
+        dfa.CouplingLayer(data, [5, 1, 2], hidden_dim_s=16, hidden_dim_t=16, rng=rng),
+        dfa.NormalizationLayer.from_data(x, -1.0, 1.0))
+    flow = dfa.Flow(chain, data)
+    state = setup(Adam(1e-3), flow)
+    p0 = trainables(chain)
+    x_tr, th_tr = data.training_data()
+    l0 = -float(dfa.nll_partial_sum(flow, x_tr, th_tr)[0].item()) / x_tr.shape[1]
+    train_(flow, data, state, epochs=5, verbose=False, rng=np.random.default_rng(1))
+    assert len(flow.train_loss) == 5 and len(flow.valid_loss) == 5
+    assert all(np.isfinite(flow.train_loss)) and all(np.isfinite(flow.valid_loss))
+    assert flow.train_loss[-1] < l0
+    # the Python model holds the trained parameters (sync_model)
+    assert not np.array_equal(trainables(chain), p0)
+    x_new = dfa.sample(flow, (2, 5, 7), (-1.0,))
+    assert tuple(x_new.shape) == (5, 2, 5, 7)
+
+
+def test_train_matches_oracle_steps(cuda):
+    """Three full train! mini-batch steps (shuffle off) against the oracle's
+    gradient + Adam restatement: parameters agree to fp32 tolerance."""
+    spec, chain, d, n = _setup("readme", seed=4)
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((5, 96)).astype(np.float32)
+    th = rng.random((1, 96)).astype(np.float32)
+    tr = HIPTrainer(chain.hip(), Adam())
+    p = trainables(chain).astype(np.float32)
+    st = [np.zeros_like(p), np.zeros_like(p), (np.float32(0.9), np.float32(0.999))]
+    ref_spec = chain.to_spec()
+    for b0 in range(0, 96, 32):
+        xb, tb = x[:, b0:b0 + 32], th[:, b0:b0 + 32]
+        import torch
+
+        tr.step(_dev(xb, cuda), _dev(tb, cuda), 32)
+        torch.cuda.synchronize()
+        _, g = O.nll_and_grad(ref_spec, xb, tb)
+        O.adam_update(p, _flat_oracle_grads(ref_spec, g).astype(np.float32), st)
+        load_trainables(chain, p)
+        ref_spec = chain.to_spec()
+    got = tr.get_params()
+    # Adam normalises the step (≈ η per coordinate); coordinates whose gradient is
+    # near zero can move by O(η) on fp32 noise, so compare at the scale of η.
+    assert np.max(np.abs(got - p)) <= 3e-4, np.max(np.abs(got - p))
+    assert np.mean(np.abs(got - p)) <= 1e-5
+
+
+def test_train_unsupported_structures(cuda):
+    rng = np.random.default_rng(0)
+    wide = dfa.FlowChain.repeat(dfa.CouplingBlock, 1, 4, hidden_dim_s=128, hidden_dim_t=128, rng=rng)
+    with pytest.raises(dfa.UnsupportedError):
+        HIPTrainer(wide.hip(), Adam())
+    sp = dfa.FlowChain(dfa.CouplingLayer(dfa.RNVPCouplingLayer, 4, 2, σ="softplus", rng=rng))
+    with pytest.raises(dfa.UnsupportedError):
+        HIPTrainer(sp.hip(), Adam())
