@@ -136,7 +136,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1 << 20, help="samples per GPU")
-    ap.add_argument("--mode", choices=["forward", "nll"], default="forward")
+    ap.add_argument("--mode", choices=["forward", "nll", "train"], default="forward")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg2",
                     help="cfg2 is the headline (BASELINE configs[1]); cfg1/cfg4 are secondary measurements")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -179,9 +179,24 @@ def main():
     ldj = torch.empty(B, device=dev)
     s64 = torch.zeros(2, dtype=torch.float64, device=dev)
 
+    trainer = None
     if args.mode == "forward":
         def step():
             hc.run("forward", zbuf, thbuf, xbuf, ldj, B)
+    elif args.mode == "train":
+        # one train! step (src/Flows.jl:398-413) on a fixed synthetic batch: inverse pass,
+        # reverse sweep, gradient all-reduce across ranks (RCCL), Adam, weight repack
+        from densityflows_amd.train import Adam, HIPTrainer
+
+        hc.run("forward", zbuf, thbuf, xbuf, ldj, B)  # data points x = forward(z)
+        trainer = HIPTrainer(hc, Adam(1e-3))
+        gview = trainer.grad() if dist is not None else None
+
+        def step():
+            trainer.gradient(xbuf, thbuf, B, B * world, s64[:1])
+            if dist is not None:
+                dist.all_reduce(gview)
+            trainer.apply()
     else:
         flow = dfa.Flow(chain, metadata=dfa.MetaData("", d, n, np.zeros(n, np.float32), np.ones(n, np.float32)))
         fh = flow.hip(device=gpu)
@@ -222,13 +237,19 @@ def main():
     flop = info.flops_per_sample * B
     achieved_tflops = flop / kernel_s / 1e12
     hbm_algo = (8.0 * d + 4.0 * n + 4.0) * B          # read z (+θ), write x, ldj
+    if args.mode == "train":
+        # algorithmic training work: forward + 2× backward (dX and dW) = 3F per sample
+        flop = 3.0 * info.flops_per_sample * B
+        achieved_tflops = flop / kernel_s / 1e12
 
     traffic = None
     if args.config == "cfg2" and args.mode == "forward" and B == (1 << 20):
         traffic = pmc_traffic(TRAFFIC_PROFILE)
     if rank == 0:
         out = {
-            "metric": METRIC if args.mode == "forward" else "NLL (inverse+logpdf+Σ, RCCL all-reduce) Msamples/s",
+            "metric": {"forward": METRIC, "nll": "NLL (inverse+logpdf+Σ, RCCL all-reduce) Msamples/s",
+                       "train": "train! step (inverse+NLL+backward+Adam, RCCL gradient all-reduce) Msamples/s"
+                       }[args.mode],
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -242,13 +263,15 @@ def main():
             "data": "synthetic: z ~ N(0,1) generated on device; random-init weights (glorot, see bench.build_chain)",
             "config": {"workload": workload + ("" if world == 1 else f"; config3 sharding {world}x"),
                        "per_gpu_batch": B, "global_batch": B * world,
-                       "parallelism": f"dp{world} (independent sample shards, no data-path collective)"
-                       if args.mode == "forward" else f"dp{world} + RCCL all-reduce of the NLL partial"},
+                       "parallelism": {"forward": f"dp{world} (independent sample shards, no data-path collective)",
+                                       "nll": f"dp{world} + RCCL all-reduce of the NLL partial",
+                                       "train": f"dp{world} + RCCL all-reduce of the flat gradient"}[args.mode]},
             "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": PEAK_F32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_F32_TFLOPS, 4),
                          "traffic": traffic,
                          "traffic_source": TRAFFIC_PROFILE if traffic is not None else None,
                          "kernel_ms": round(kernel_s * 1e3, 4),
+                         "kernel_ms_scope": "whole step (all launches)" if args.mode == "train" else "one launch",
                          "algorithmic_flop_per_sample": info.flops_per_sample,
                          "hbm_algorithmic_GBps": round(hbm_algo / kernel_s / 1e9, 2)},
         }

@@ -565,6 +565,14 @@ chain_kernel(ChainArgs a) {
             }
         }
         have_acc = have_acc || last_in_elem;
+        if (!FWD && a.snap) {  // training: keep every layer's output for the reverse sweep
+            float* dst = a.snap + (int64_t)li * a.batch * d;
+            for (int tt = 0; tt < nt; ++tt) {
+                const int smp = (wave * nt + tt) * 16 + j;
+                if (smp < nvalid)
+                    for (int i = g; i < d; i += 4) dst[(s0 + smp) * d + i] = sm.state[row_of(tt) + n + i];
+            }
+        }
     }
 
     // ---- epilogue ----

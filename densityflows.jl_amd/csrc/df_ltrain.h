@@ -1,0 +1,86 @@
+// df_ltrain.h — layer-wise training path for conditioners the fused per-net
+// kernel (df_train_impl.h) cannot hold in registers (hidden width > 64, more
+// than one hidden Dense, > 4 transformed dims; BASELINE config 5: d = 32,
+// hidden 256).
+//
+// Per conditioner net, every Dense becomes one MFMA GEMM over the whole batch
+// with a fused epilogue; activations live in HBM in the sample-major layout
+// (Julia's (h, B) column-major: sample j's h values contiguous), which is
+// exactly the register layout of an MFMA accumulator tile, so loads and stores
+// are 16-byte vectors:
+//   forward   H0 = σ0(W0 x + b0) (x gathered from vcat(θ, u)[axis_nn], kept),
+//             Hk = σk(Wk Hk-1 + bk),  Y = σo(Wo H + bo)
+//             → coupling pullback in the epilogue → ȳ  (s̄ / t̄, ū_af)
+//   backward  δ = (Wᵀ ȳ) ⊙ σ'(H) per Dense, x̄ = W0ᵀ δ0 → z̄ of identity dims
+//   weights   dW = δ · inᵀ, db = Σ δ: split-K over samples, one partial per
+//             workgroup (fixed-order reduction afterwards, as the fused path).
+// Weight fragments (W and Wᵀ, [kq][m][lane][4]) are streamed through two LDS
+// chunk buffers shared by the 8 waves of a workgroup.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "df_plan.h"
+
+namespace df {
+
+enum : int { LIN_BUF = 0, LIN_GATHER = 1 };
+enum : int { LEPI_ACT = 0, LEPI_COUPLE = 1, LEPI_DACT = 2, LEPI_XBAR = 3 };
+
+constexpr int kLChunkBytes = 32 * 1024;  // weight chunk (LDS, double-buffered)
+constexpr int kLTiles = 2;               // 16-sample tiles per wave per round
+constexpr int kLdwSamples = 32;          // samples per dW staging step
+constexpr int kLdwStride = kLdwSamples + 4;
+constexpr int kLdwMaxBlocks = 32;        // 16×16 output blocks per wave (registers)
+
+struct LDenseArgs {
+    const uint8_t* wfrag;   // fragments [kq][m][lane][4] of A (M = 16·MT rows)
+    const float* bias;      // 16·MT floats or nullptr
+    int nkq, chunk_kq;
+    int act;                // LEPI_ACT / LEPI_COUPLE: σ of this Dense
+    // B operand
+    const float* in;        // LIN_BUF: [B][ld_in]
+    int ld_in;
+    const float* theta;     // LIN_GATHER: vcat(θ, u)[axis_nn] features
+    const float* tmin;
+    const float* tmax;
+    const float* u_in;
+    const int32_t* feat;    // feature → state slot (n + d: zero)
+    int n_in;               // true conditioner input width (gather / xbar)
+    float* xsave;           // LIN_GATHER: gathered features stored [B][ld_x] (may be nullptr)
+    int ld_x;
+    // epilogue
+    float* out;             // [B][ld_out]
+    int ld_out;
+    const float* hprev;     // LEPI_DACT: σ'(hprev) with activation dact
+    int ld_h, dact;
+    float* zbar;            // LEPI_COUPLE / LEPI_XBAR
+    const float* u_out;
+    float* ebuf;            // [B][32] exp(-s)
+    const int32_t* af;
+    int n_af, phase, kind;
+    float inv_n;
+    int64_t batch;
+    int d, n;
+};
+
+struct LdwArgs {
+    const float* da;        // δ  [B][lda] (rows = Dense outputs)
+    int lda, m_true;
+    const float* xb;        // in [B][ldb] (rows = Dense inputs)
+    int ldb, n_true;
+    int mta, ntb;           // 16-row tiles of each operand
+    float* partial;         // [workgroup][p_total]
+    int64_t p_total;
+    int w_off, b_off;       // trainables offsets (b_off -1: no bias)
+    int64_t batch;
+};
+
+hipError_t launch_ldense(int mt, int in_kind, int epi, const LDenseArgs& a, unsigned grid, size_t lds,
+                         hipStream_t st);
+hipError_t ldense_occupancy(int mt, int in_kind, int epi, size_t lds, int* blocks);
+hipError_t set_ldense_lds_limit(size_t lds);
+hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st);
+size_t ldw_lds_bytes();
+
+}  // namespace df

@@ -1,0 +1,319 @@
+// df_ltrain.hip — kernels of the layer-wise training path (df_ltrain.h).
+#include "df_chain_impl.h"
+#include "df_ltrain.h"
+#include "df_train_impl.h"
+
+namespace df {
+
+namespace {
+
+using impl::lds4;
+using impl::mfma4;
+
+__device__ __forceinline__ float gather_feature(const LDenseArgs& a, int slot, int64_t s) {
+    if (slot < a.n) {
+        float v = a.theta[s * a.n + slot];
+        if (a.tmin) {  // normalize_input (Data.jl:213-218)
+            const float lo = a.tmin[slot], diff = a.tmax[slot] - lo;
+            v = (diff == 0.f) ? 0.f : (v - lo) / diff;
+        }
+        return v;
+    }
+    if (slot < a.n + a.d) return a.u_in[s * a.d + (slot - a.n)];
+    return 0.f;
+}
+
+// One Dense over the whole batch: acc = A · in, A = packed W or Wᵀ (16·MT rows),
+// then the fused epilogue.  Persistent workgroups; each wave owns kLTiles
+// 16-sample tiles per round; A is streamed through two LDS chunk buffers.
+template <int MT, int IN, int EPI>
+__global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int T = kLTiles;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, j = lane & 15;
+    const int chunk_bytes = a.chunk_kq * MT * 1024;
+    const int nchunks = (a.nkq + a.chunk_kq - 1) / a.chunk_kq;
+    const int64_t ntiles = (a.batch + 15) / 16;
+    const int64_t per_round = (int64_t)gridDim.x * kWavesPerBlock * T;
+    const int64_t rounds = (ntiles + per_round - 1) / per_round;
+    const int64_t total = rounds * nchunks;
+
+    auto dma = [&](int c, uint8_t* dst) {
+        const int kq0 = c * a.chunk_kq;
+        const int kq1 = (kq0 + a.chunk_kq < a.nkq) ? kq0 + a.chunk_kq : a.nkq;
+        const uint8_t* src = a.wfrag + (size_t)kq0 * MT * 1024;
+        const int nk = (kq1 - kq0) * MT;  // KiB
+        for (int q = wave; q < nk; q += kWavesPerBlock)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (q << 10) + lane * 16),
+                                             (__attribute__((address_space(3))) void*)(dst + (q << 10)), 16, 0,
+                                             0);
+    };
+    dma(0, smem);
+    if (nchunks == 1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    int64_t i = 0;
+    for (int64_t r = 0; r < rounds; ++r) {
+        const int64_t t0 = ((r * gridDim.x + blockIdx.x) * kWavesPerBlock + wave) * T;
+        int64_t smp[T];
+        bool valid[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            smp[t] = (t0 + t) * 16 + j;
+            valid[t] = smp[t] < a.batch;
+        }
+        f32x4 acc[T][MT];
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+        for (int c = 0; c < nchunks; ++c, ++i) {
+            const uint8_t* buf = smem;
+            if (nchunks > 1) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk i landed (this wave's part)
+                __syncthreads();                                     // ... all parts; buffer (i+1)&1 free
+                if (i + 1 < total) dma((int)((i + 1) % nchunks), smem + (((i + 1) & 1) ? chunk_bytes : 0));
+                buf = smem + ((i & 1) ? chunk_bytes : 0);
+            }
+            const int kq0 = c * a.chunk_kq;
+            const int kq1 = (kq0 + a.chunk_kq < a.nkq) ? kq0 + a.chunk_kq : a.nkq;
+            for (int kq = kq0; kq < kq1; ++kq) {
+                f32x4 x[T];
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    if constexpr (IN == LIN_BUF) {
+                        x[t] = valid[t] ? *reinterpret_cast<const f32x4*>(a.in + smp[t] * a.ld_in + 16 * kq + 4 * g)
+                                        : f32x4{0.f, 0.f, 0.f, 0.f};
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const int f = 16 * kq + 4 * g + q;
+                            x[t][q] = (valid[t] && f < a.n_in) ? gather_feature(a, a.feat[f], smp[t]) : 0.f;
+                        }
+                        if (a.xsave && valid[t])
+                            *reinterpret_cast<f32x4*>(a.xsave + smp[t] * a.ld_x + 16 * kq + 4 * g) = x[t];
+                    }
+                }
+                const uint8_t* wb = buf + (kq - kq0) * MT * 1024 + lane * 16;
+#pragma unroll
+                for (int m = 0; m < MT; ++m) {
+                    const f32x4 w = lds4(wb + m * 1024);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+#pragma unroll
+                        for (int t = 0; t < T; ++t) acc[t][m] = mfma4(w[q], x[t][q], acc[t][m]);
+                }
+            }
+        }
+
+        // ---- epilogue: rows 16m + 4g + q of sample smp[t] ----
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            if (!valid[t]) continue;
+            const int64_t s = smp[t];
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const int row0 = 16 * m + 4 * g;
+                f32x4 v = acc[t][m];
+                if constexpr (EPI == LEPI_ACT || EPI == LEPI_COUPLE) {
+                    if (a.bias) v = v + *reinterpret_cast<const f32x4*>(a.bias + row0);  // W*x .+ b
+                    if (a.act != DF_ACT_IDENTITY)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) v[q] = impl::act_fn(a.act, v[q]);
+                }
+                if constexpr (EPI == LEPI_ACT) {
+                    *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = v;
+                } else if constexpr (EPI == LEPI_COUPLE) {
+                    // coupling pullback, rrule(RNVP_backward) src/affine/RNVP.jl:133-139
+                    f32x4 dy = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int row = row0 + q;
+                        if (row < a.n_af) {
+                            const int dim = a.af[row] - a.n;
+                            const float zb = a.zbar[s * a.d + dim];
+                            float dq;
+                            if (a.phase == TR_PHASE_S) {
+                                a.ebuf[s * 32 + row] = expf(-v[q]);
+                                dq = -zb * a.u_out[s * a.d + dim] + a.inv_n;  // s̄ = -z̄_af·z_af - j̄
+                            } else {
+                                const bool rnvp = (a.kind == DF_LAYER_RNVP);
+                                const float e = rnvp ? a.ebuf[s * 32 + row] : 1.f;
+                                dq = -zb * e;                                   // t̄ = -z̄_af·exp(-s)
+                                if (rnvp) a.zbar[s * a.d + dim] = zb * e;       // ū_af = z̄_af·exp(-s)
+                            }
+                            if (a.act != DF_ACT_IDENTITY) dq = dq * trn::act_grad(a.act, v[q]);
+                            dy[q] = dq;
+                        }
+                    }
+                    *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = dy;
+                } else if constexpr (EPI == LEPI_DACT) {
+                    const f32x4 h = *reinterpret_cast<const f32x4*>(a.hprev + s * a.ld_h + row0);
+                    if (a.dact == DF_ACT_RELU) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) v[q] = (h[q] > 0.f) ? v[q] : 0.f;
+                    } else if (a.dact != DF_ACT_IDENTITY) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) v[q] = v[q] * trn::act_grad(a.dact, h[q]);
+                    }
+                    *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = v;
+                } else {  // LEPI_XBAR: conditioner-input gradient into z̄ of identity dims
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int f = row0 + q;
+                        if (f < a.n_in) {
+                            const int slot = a.feat[f];
+                            if (slot >= a.n && slot < a.n + a.d) a.zbar[s * a.d + (slot - a.n)] += v[q];
+                        }
+                    }
+                }
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// dW = δ · inᵀ and db = Σ δ over this workgroup's contiguous sample range;
+// both operands staged transposed in LDS ([row][sample]); output 16×16 blocks
+// are dealt round-robin to the 8 waves and accumulated in registers.
+__global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    float* TA = lsm;
+    float* TB = lsm + 256 * kLdwStride;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, j = lane & 15;
+    const int MA = 16 * a.mta, NB = 16 * a.ntb;
+    const int nblocks = a.mta * a.ntb;
+    const int64_t per = (a.batch + gridDim.x - 1) / gridDim.x;
+    const int64_t s_begin = (int64_t)blockIdx.x * per;
+    const int64_t s_end = (s_begin + per < a.batch) ? s_begin + per : a.batch;
+
+    f32x4 acc[kLdwMaxBlocks / 1];
+    float db[kLdwMaxBlocks];
+#pragma unroll
+    for (int q = 0; q < kLdwMaxBlocks; ++q) {
+        acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        db[q] = 0.f;
+    }
+
+    for (int64_t s0 = s_begin; s0 < s_end; s0 += kLdwSamples) {
+        __syncthreads();
+        // stage [rows][32 samples] of both operands (zero beyond the range)
+        const int qa = MA / 4, qb = NB / 4;
+        for (int e = tid; e < kLdwSamples * qa; e += kBlockThreads) {
+            const int ss = e / qa, rq = e - ss * qa;
+            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (s0 + ss < s_end) v = *reinterpret_cast<const f32x4*>(a.da + (s0 + ss) * a.lda + 4 * rq);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) TA[(4 * rq + q) * kLdwStride + ss] = v[q];
+        }
+        for (int e = tid; e < kLdwSamples * qb; e += kBlockThreads) {
+            const int ss = e / qb, rq = e - ss * qb;
+            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (s0 + ss < s_end) v = *reinterpret_cast<const f32x4*>(a.xb + (s0 + ss) * a.ldb + 4 * rq);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) TB[(4 * rq + q) * kLdwStride + ss] = v[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kLdwSamples / 16; ++u) {
+#pragma unroll
+            for (int q = 0; q < kLdwMaxBlocks; ++q) {
+                const int b = wave + kWavesPerBlock * q;
+                if (b < nblocks) {
+                    const int ma = b / a.ntb, nb = b - ma * a.ntb;
+                    const f32x4 fa = *reinterpret_cast<const f32x4*>(TA + (16 * ma + j) * kLdwStride + 16 * u + 4 * g);
+                    const f32x4 fb = *reinterpret_cast<const f32x4*>(TB + (16 * nb + j) * kLdwStride + 16 * u + 4 * g);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[q] = mfma4(fa[k], fb[k], acc[q]);
+                    if (nb == 0) db[q] += trn::hsum4(fa);
+                }
+            }
+        }
+    }
+
+    float* dst = a.partial + (int64_t)blockIdx.x * a.p_total;
+#pragma unroll
+    for (int q = 0; q < kLdwMaxBlocks; ++q) {
+        const int b = wave + kWavesPerBlock * q;
+        if (b < nblocks) {
+            const int ma = b / a.ntb, nb = b - ma * a.ntb;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * ma + 4 * g + r, col = 16 * nb + j;
+                if (row < a.m_true && col < a.n_true) dst[a.w_off + row + (int64_t)a.m_true * col] = acc[q][r];
+            }
+            if (nb == 0) {
+                const float v = uni::xgroup_sum(db[q]);
+                if (g == 0 && a.b_off >= 0 && 16 * ma + j < a.m_true) dst[a.b_off + 16 * ma + j] = v;
+            }
+        }
+    }
+}
+
+template <int MT>
+void* ldense_ptr_mt(int in_kind, int epi) {
+    if (in_kind == LIN_GATHER) return reinterpret_cast<void*>(&ldense_kernel<MT, LIN_GATHER, LEPI_ACT>);
+    switch (epi) {
+        case LEPI_ACT: return reinterpret_cast<void*>(&ldense_kernel<MT, LIN_BUF, LEPI_ACT>);
+        case LEPI_COUPLE: return reinterpret_cast<void*>(&ldense_kernel<MT, LIN_BUF, LEPI_COUPLE>);
+        case LEPI_DACT: return reinterpret_cast<void*>(&ldense_kernel<MT, LIN_BUF, LEPI_DACT>);
+        default: return reinterpret_cast<void*>(&ldense_kernel<MT, LIN_BUF, LEPI_XBAR>);
+    }
+}
+
+void* ldense_ptr(int mt, int in_kind, int epi) {
+    switch (mt) {
+        case 1: return ldense_ptr_mt<1>(in_kind, epi);
+        case 2: return ldense_ptr_mt<2>(in_kind, epi);
+        case 4: return ldense_ptr_mt<4>(in_kind, epi);
+        case 8: return ldense_ptr_mt<8>(in_kind, epi);
+        case 16: return ldense_ptr_mt<16>(in_kind, epi);
+        default: return nullptr;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_ldense(int mt, int in_kind, int epi, const LDenseArgs& a, unsigned grid, size_t lds,
+                         hipStream_t st) {
+    void* k = ldense_ptr(mt, in_kind, epi);
+    if (!k) return hipErrorInvalidValue;
+    void* args[] = {const_cast<LDenseArgs*>(&a)};
+    return hipLaunchKernel(k, dim3(grid), dim3(kBlockThreads), args, lds, st);
+}
+
+hipError_t ldense_occupancy(int mt, int in_kind, int epi, size_t lds, int* blocks) {
+    void* k = ldense_ptr(mt, in_kind, epi);
+    if (!k) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k, kBlockThreads, lds);
+}
+
+hipError_t set_ldense_lds_limit(size_t lds) {
+    for (int mt : {1, 2, 4, 8, 16}) {
+        for (int epi = 0; epi < 4; ++epi) {
+            hipError_t e = hipFuncSetAttribute(ldense_ptr(mt, LIN_BUF, epi),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipFuncSetAttribute(ldense_ptr(mt, LIN_GATHER, LEPI_ACT),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    return hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)ldw_lds_bytes());
+}
+
+size_t ldw_lds_bytes() { return (size_t)2 * 256 * kLdwStride * 4; }
+
+hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st) {
+    void* args[] = {const_cast<LdwArgs*>(&a)};
+    return hipLaunchKernel(reinterpret_cast<void*>(&ldw_kernel), dim3(grid), dim3(kBlockThreads), args,
+                           ldw_lds_bytes(), st);
+}
+
+}  // namespace df

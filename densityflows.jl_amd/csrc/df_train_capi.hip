@@ -6,10 +6,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
 #include "df_handle.h"
+#include "df_ltrain.h"
 #include "df_train.h"
 
 using namespace df;
@@ -24,6 +26,31 @@ struct SweepOp {
 };
 
 int round16(int v) { return (v + 15) / 16 * 16; }
+
+int pow2_tiles(int rows) {
+    int t = 1;
+    while (16 * t < rows) t *= 2;
+    return t;
+}
+
+// Layer-wise path: one packed GEMM operand (W or Wᵀ) of one Dense.
+struct LOp {
+    int mt = 0;              // output row tiles (power of two <= 16)
+    int nkq = 0;             // k-quads of the contraction
+    int chunk_kq = 1;        // k-quads per LDS chunk
+    int64_t frag = 0;        // byte offset in the layer-wise blob
+    int64_t bias = -1;       // float offset of the padded bias (forward only)
+};
+
+struct LDense {
+    int in_dim = 0, out_dim = 0, act = 0;
+    int w_off = 0, b_off = -1;
+    LOp fwd, bwd;            // acc = W·in (out rows) ; acc = Wᵀ·δ (in rows)
+};
+
+struct LNet {
+    std::vector<LDense> dn;  // Dense(in,h,σ0), hidden..., Dense(h,out,σo)
+};
 
 bool act_trainable(int a) {
     return a == DF_ACT_IDENTITY || a == DF_ACT_RELU || a == DF_ACT_TANH || a == DF_ACT_SIGMOID;
@@ -59,15 +86,119 @@ struct df_train {
     int64_t cap = 0;       // batch capacity of snap / zbar / ebuf
     int grid = 0;          // workgroups of a full net launch (resident on the device)
     size_t lds_max = 0;
+    // layer-wise path (hidden width > 64, deep or wide-output conditioners)
+    bool layerwise = false;
+    std::vector<LNet> lnets;
+    std::vector<uint8_t> lblob;      // fragments (W and Wᵀ) then padded biases
+    std::vector<int32_t> ldst, lsrc; // repack map (float index ← trainables index)
+    void* d_lblob = nullptr;
+    void* d_ldst = nullptr;
+    void* d_lsrc = nullptr;
+    int lgrid = 0;                   // workgroups of the dW kernels (partial rows)
+    int lwidth = 16;                 // widest activation row (floats)
+    int lmax_h = 1;                  // activation buffers needed (hidden Denses + 1)
+    std::vector<float*> d_lh, d_ld; // H_k and δ_k buffers [cap][lwidth]
+    float* d_ly = nullptr;           // ȳ  [cap][lwidth]
+    float* d_lx = nullptr;           // gathered conditioner input [cap][lwidth]
 };
 
 namespace {
 
 void free_all(df_train* t) {
-    void* ptrs[] = {t->d_params, t->d_m, t->d_v,  t->d_grad, t->d_partial, t->d_tblob, t->d_pdst,
-                    t->d_psrc,   t->d_tdst, t->d_tsrc, t->d_snap, t->d_zbar,  t->d_ebuf,  t->d_lpsum};
+    void* ptrs[] = {t->d_params, t->d_m,    t->d_v,    t->d_grad, t->d_partial, t->d_tblob, t->d_pdst,
+                    t->d_psrc,   t->d_tdst, t->d_tsrc, t->d_snap, t->d_zbar,    t->d_ebuf,  t->d_lpsum,
+                    t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_ly,   t->d_lx};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    for (float* p : t->d_lh)
+        if (p) (void)hipFree(p);
+    for (float* p : t->d_ld)
+        if (p) (void)hipFree(p);
+}
+
+// Pack A = W (transposed = false: rows = out, k = in) or Wᵀ (rows = in, k = out)
+// as fragments [kq][m][lane][4]: A[16m + (lane&15)][16kq + 4(lane>>4) + r].
+LOp pack_lop(df_train* t, const Plan& P, const LDense& D, bool transposed) {
+    LOp op;
+    const int rows = transposed ? D.in_dim : D.out_dim;
+    const int kdim = transposed ? D.out_dim : D.in_dim;
+    op.mt = pow2_tiles(rows);
+    op.nkq = (kdim + 15) / 16;
+    op.chunk_kq = std::max(1, kLChunkBytes / (op.mt * 1024));
+    op.frag = (int64_t)t->lblob.size();
+    const size_t bytes = (size_t)op.nkq * op.mt * 1024;
+    t->lblob.resize(t->lblob.size() + bytes, 0);
+    float* f = reinterpret_cast<float*>(t->lblob.data() + op.frag);
+    const int64_t f0 = op.frag / 4;
+    for (int kq = 0; kq < op.nkq; ++kq)
+        for (int m = 0; m < op.mt; ++m)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * m + (lane & 15), k = 16 * kq + 4 * (lane >> 4) + r;
+                    if (i >= rows || k >= kdim) continue;
+                    const int orow = transposed ? k : i, icol = transposed ? i : k;  // W[orow, icol]
+                    const int64_t src = D.w_off + orow + (int64_t)D.out_dim * icol;
+                    const int64_t q = (((int64_t)kq * op.mt + m) * 64 + lane) * 4 + r;
+                    f[q] = P.trainables[src];
+                    t->ldst.push_back((int32_t)(f0 + q));
+                    t->lsrc.push_back((int32_t)src);
+                }
+    return op;
+}
+
+void pack_lbias(df_train* t, const Plan& P, const LDense& D, LOp& op) {
+    if (D.b_off < 0) return;
+    op.bias = (int64_t)t->lblob.size() / 4;
+    t->lblob.resize(t->lblob.size() + (size_t)op.mt * 64, 0);
+    float* f = reinterpret_cast<float*>(t->lblob.data()) + op.bias;
+    for (int r = 0; r < D.out_dim; ++r) {
+        f[r] = P.trainables[D.b_off + r];
+        t->ldst.push_back((int32_t)(op.bias + r));
+        t->lsrc.push_back(D.b_off + r);
+    }
+}
+
+int build_lnets(df_train* t) {
+    const Plan& P = t->c->plan;
+    t->ops.clear();
+    t->lnets.clear();
+    for (int li = 0; li < P.n_layers; ++li) {
+        const DevLayer& L = P.layers[li];
+        if (L.kind == DF_LAYER_NORM) {
+            t->ops.push_back({li, -1, TR_PHASE_T});
+            continue;
+        }
+        auto add = [&](int d0, int nd, int phase) -> int {
+            LNet net;
+            for (int k = 0; k < nd; ++k) {
+                const DevDense& DD = P.denses[d0 + k];
+                if (!act_trainable(DD.act))
+                    return set_err(DF_ERR_UNSUPPORTED, "training supports σ ∈ {identity, relu, tanh, sigmoid}");
+                LDense D;
+                D.in_dim = DD.in_dim;
+                D.out_dim = DD.n_out;
+                D.act = DD.act;
+                D.w_off = DD.w_off;
+                D.b_off = DD.b_off;
+                D.fwd = pack_lop(t, P, D, false);
+                pack_lbias(t, P, D, D.fwd);
+                D.bwd = pack_lop(t, P, D, true);
+                t->lwidth = std::max({t->lwidth, 16 * D.fwd.mt, 16 * D.bwd.mt});
+                net.dn.push_back(D);
+            }
+            if (nd < 2) return set_err(DF_ERR_UNSUPPORTED, "training needs conditioners of >= 2 Dense layers");
+            t->lmax_h = std::max(t->lmax_h, nd - 1);
+            t->lnets.push_back(net);
+            t->ops.push_back({li, (int)t->lnets.size() - 1, phase});
+            return DF_OK;
+        };
+        int rc = DF_OK;
+        if (L.kind == DF_LAYER_RNVP) rc = add(L.s_dense0, L.s_ndense, TR_PHASE_S);
+        if (rc == DF_OK) rc = add(L.t_dense0, L.t_ndense, TR_PHASE_T);
+        if (rc != DF_OK) return rc;
+    }
+    t->lblob.resize(t->lblob.size() + 16, 0);
+    return DF_OK;
 }
 
 // Transposed fragments of one net (W0ᵀ, W_hᵀ) appended to t->tblob with
@@ -185,10 +316,37 @@ int ensure_capacity(df_train* t, int64_t batch) {
         }
     t->cap = 0;
     const int64_t cap = std::max<int64_t>(batch, 1024);
+    for (float** p : {&t->d_ly, &t->d_lx})
+        if (*p) {
+            (void)hipFree(*p);
+            *p = nullptr;
+        }
+    for (auto* v : {&t->d_lh, &t->d_ld}) {
+        for (float* p : *v)
+            if (p) (void)hipFree(p);
+        v->clear();
+    }
+    const int ew = t->layerwise ? 32 : 4;  // exp(-s) row width
     if (hipMalloc(reinterpret_cast<void**>(&t->d_snap), sizeof(float) * P.n_layers * cap * P.d) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&t->d_zbar), sizeof(float) * cap * P.d) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&t->d_ebuf), sizeof(float) * cap * 4) != hipSuccess)
+        hipMalloc(reinterpret_cast<void**>(&t->d_ebuf), sizeof(float) * cap * ew) != hipSuccess)
         return set_err(DF_ERR_NOMEM, "hipMalloc failed (training activations)");
+    if (t->layerwise) {
+        const size_t row = sizeof(float) * (size_t)cap * t->lwidth;
+        if (hipMalloc(reinterpret_cast<void**>(&t->d_ly), row) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&t->d_lx), row) != hipSuccess)
+            return set_err(DF_ERR_NOMEM, "hipMalloc failed (training activations)");
+        for (int k = 0; k <= t->lmax_h; ++k) {
+            float *h = nullptr, *dl = nullptr;
+            if (hipMalloc(reinterpret_cast<void**>(&h), row) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void**>(&dl), row) != hipSuccess) {
+                if (h) (void)hipFree(h);
+                return set_err(DF_ERR_NOMEM, "hipMalloc failed (training activations)");
+            }
+            t->d_lh.push_back(h);
+            t->d_ld.push_back(dl);
+        }
+    }
     t->cap = cap;
     return DF_OK;
 }
@@ -198,10 +356,122 @@ int repack(df_train* t, hipStream_t st) {
     const Plan& P = c->plan;
     hipError_t e = launch_repack(static_cast<float*>(c->d_blob), static_cast<const int32_t*>(t->d_pdst),
                                  static_cast<const int32_t*>(t->d_psrc), (int64_t)P.pack_dst.size(), t->d_params, st);
-    if (e == hipSuccess)
+    if (e == hipSuccess && !t->tdst.empty())
         e = launch_repack(static_cast<float*>(t->d_tblob), static_cast<const int32_t*>(t->d_tdst),
                           static_cast<const int32_t*>(t->d_tsrc), (int64_t)t->tdst.size(), t->d_params, st);
+    if (e == hipSuccess && !t->ldst.empty())
+        e = launch_repack(static_cast<float*>(t->d_lblob), static_cast<const int32_t*>(t->d_ldst),
+                          static_cast<const int32_t*>(t->d_lsrc), (int64_t)t->ldst.size(), t->d_params, st);
     return e == hipSuccess ? DF_OK : hip_err(e, "repack kernel launch");
+}
+
+// Reverse sweep of the layer-wise path (chain order; see df_ltrain.h).
+int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float inv_n, bool flow, hipStream_t st) {
+    df_chain* c = t->c;
+    const Plan& P = c->plan;
+    const int64_t bd = batch * P.d;
+    const int64_t ntiles = (batch + 15) / 16;
+    const unsigned dgrid =
+        (unsigned)std::max<int64_t>(1, std::min<int64_t>(c->n_cu, (ntiles + kWavesPerBlock * kLTiles - 1) /
+                                                                          (kWavesPerBlock * kLTiles)));
+    const int W = t->lwidth;
+    const uint8_t* lb = static_cast<const uint8_t*>(t->d_lblob);
+    const float* lbf = static_cast<const float*>(t->d_lblob);
+    hipError_t e = hipSuccess;
+    auto dense = [&](const LOp& op, int in_kind, int epi, LDenseArgs a) {
+        a.wfrag = lb + op.frag;
+        a.bias = (op.bias >= 0 && (epi == LEPI_ACT || epi == LEPI_COUPLE)) ? lbf + op.bias : nullptr;
+        a.nkq = op.nkq;
+        a.chunk_kq = op.chunk_kq;
+        const int nchunks = (op.nkq + op.chunk_kq - 1) / op.chunk_kq;
+        const size_t lds = (size_t)(nchunks > 1 ? 2 : 1) * std::min(op.nkq, op.chunk_kq) * op.mt * 1024;
+        if (e == hipSuccess) e = launch_ldense(op.mt, in_kind, epi, a, dgrid, lds, st);
+    };
+    for (const SweepOp& op : t->ops) {
+        const DevLayer& L = P.layers[op.layer];
+        if (op.net < 0) {
+            const float* xmn = static_cast<const float*>(c->d_params) + L.norm_off;
+            e = launch_norm_adjoint(t->d_zbar, xmn, xmn + P.d, L.alpha, L.beta, P.d, batch, st);
+            if (e != hipSuccess) return hip_err(e, "norm adjoint launch");
+            continue;
+        }
+        const LNet& N = t->lnets[op.net];
+        const int nd = (int)N.dn.size();
+        LDenseArgs b{};
+        b.theta = theta;
+        b.tmin = flow ? c->d_bounds : nullptr;
+        b.tmax = flow ? c->d_bounds + P.n : nullptr;
+        b.u_in = (op.layer + 1 < P.n_layers) ? t->d_snap + (int64_t)(op.layer + 1) * bd : x;
+        b.u_out = t->d_snap + (int64_t)op.layer * bd;
+        b.feat = static_cast<const int32_t*>(c->d_tables) + L.feat_tab;
+        b.af = static_cast<const int32_t*>(c->d_tables) + L.af_tab;
+        b.n_in = N.dn[0].in_dim;
+        b.zbar = t->d_zbar;
+        b.ebuf = t->d_ebuf;
+        b.n_af = L.n_af;
+        b.phase = op.phase;
+        b.kind = L.kind;
+        b.inv_n = inv_n;
+        b.batch = batch;
+        b.d = P.d;
+        b.n = P.n;
+        b.ld_in = b.ld_out = b.ld_h = b.ld_x = W;
+        // forward recompute: H_k = σ(W_k · in + b_k), then the output Dense + coupling pullback → ȳ
+        for (int k = 0; k < nd; ++k) {
+            LDenseArgs a = b;
+            a.act = N.dn[k].act;
+            if (k == 0) {
+                a.xsave = t->d_lx;
+            } else {
+                a.in = t->d_lh[k - 1];
+            }
+            if (k + 1 < nd) {
+                a.out = t->d_lh[k];
+                dense(N.dn[k].fwd, k == 0 ? LIN_GATHER : LIN_BUF, LEPI_ACT, a);
+            } else {
+                a.out = t->d_ly;
+                dense(N.dn[k].fwd, LIN_BUF, LEPI_COUPLE, a);
+            }
+        }
+        // backward: δ_{k-1} = (W_kᵀ δ_k) ⊙ σ'(H_{k-1}); x̄ = W0ᵀ δ_0 → z̄ (identity dims)
+        const float* gcur = t->d_ly;
+        for (int k = nd - 1; k >= 1; --k) {
+            LDenseArgs a = b;
+            a.in = gcur;
+            a.hprev = t->d_lh[k - 1];
+            a.dact = N.dn[k - 1].act;
+            a.out = t->d_ld[k - 1];
+            dense(N.dn[k].bwd, LIN_BUF, LEPI_DACT, a);
+            gcur = t->d_ld[k - 1];
+        }
+        {
+            LDenseArgs a = b;
+            a.in = gcur;
+            dense(N.dn[0].bwd, LIN_BUF, LEPI_XBAR, a);
+        }
+        if (e != hipSuccess) return hip_err(e, "layer-wise dense launch");
+        // dW = δ · inᵀ, db = Σ δ (per-workgroup partials)
+        for (int k = 0; k < nd; ++k) {
+            const LDense& D = N.dn[k];
+            LdwArgs w{};
+            w.da = (k + 1 == nd) ? t->d_ly : t->d_ld[k];
+            w.lda = W;
+            w.m_true = D.out_dim;
+            w.mta = D.fwd.mt;
+            w.xb = (k == 0) ? t->d_lx : t->d_lh[k - 1];
+            w.ldb = W;
+            w.n_true = D.in_dim;
+            w.ntb = D.bwd.mt;
+            w.partial = t->d_partial;
+            w.p_total = t->P;
+            w.w_off = D.w_off;
+            w.b_off = D.b_off;
+            w.batch = batch;
+            e = launch_ldw(w, (unsigned)t->lgrid, st);
+            if (e != hipSuccess) return hip_err(e, "dW kernel launch");
+        }
+    }
+    return DF_OK;
 }
 
 }  // namespace
@@ -234,7 +504,19 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
     const Plan& P = c->plan;
     t->P = (int64_t)P.trainables.size();
     t->relu = P.relu_only;
-    int rc = build_nets(t);
+    // fused per-net kernel when every conditioner fits its registers, else layer-wise
+    const char* force = std::getenv("DF_TRAIN_LAYERWISE");
+    int rc = (force && force[0] == '1') ? DF_ERR_UNSUPPORTED : build_nets(t);
+    if (rc == DF_ERR_UNSUPPORTED) {
+        t->nets.clear();
+        t->net_nh.clear();
+        t->ops.clear();
+        t->tblob.clear();
+        t->tdst.clear();
+        t->tsrc.clear();
+        t->layerwise = true;
+        rc = build_lnets(t);
+    }
     if (rc != DF_OK) {
         delete t;
         return rc;
@@ -263,6 +545,15 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
             occ = (i == 0) ? b : std::min(occ, b);
     }
     t->grid = std::max(1, c->n_cu * occ);
+    if (t->layerwise) {
+        e = set_ldense_lds_limit((size_t)2 * kLChunkBytes);
+        if (e != hipSuccess) {
+            df_train_destroy(t);
+            return hip_err(e, "hipFuncSetAttribute(layer-wise training)");
+        }
+        t->lgrid = std::max(1, c->n_cu);
+        t->grid = t->lgrid;  // partial rows
+    }
     const size_t pb = sizeof(float) * (size_t)std::max<int64_t>(t->P, 4);
     if (hipMalloc(reinterpret_cast<void**>(&t->d_params), pb) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&t->d_m), pb) != hipSuccess ||
@@ -273,7 +564,9 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
         df_train_destroy(t);
         return set_err(DF_ERR_NOMEM, "hipMalloc failed (training state)");
     }
-    if ((rc = upload(t->tblob, &t->d_tblob)) != DF_OK || (rc = upload(P.pack_dst, &t->d_pdst)) != DF_OK ||
+    if ((rc = upload(t->tblob, &t->d_tblob)) != DF_OK || (rc = upload(t->lblob, &t->d_lblob)) != DF_OK ||
+        (rc = upload(t->ldst, &t->d_ldst)) != DF_OK || (rc = upload(t->lsrc, &t->d_lsrc)) != DF_OK ||
+        (rc = upload(P.pack_dst, &t->d_pdst)) != DF_OK ||
         (rc = upload(P.pack_src, &t->d_psrc)) != DF_OK || (rc = upload(t->tdst, &t->d_tdst)) != DF_OK ||
         (rc = upload(t->tsrc, &t->d_tsrc)) != DF_OK) {
         std::string m = last_error();
@@ -336,6 +629,12 @@ int df_train_gradient(df_train* t, const float* x, const float* theta_raw, int64
     hipError_t e = launch_scale(t->d_zbar, t->d_snap, inv_n, bd, st);
     if (e != hipSuccess) return hip_err(e, "scale kernel launch");
     // 3. reverse sweep, chain order
+    if (t->layerwise) {
+        rc = lsweep(t, x, theta_raw, batch, inv_n, flow, st);
+        if (rc != DF_OK) return rc;
+        e = launch_reduce_grads(t->d_partial, t->lgrid, t->P, t->d_grad, st);
+        return e == hipSuccess ? DF_OK : hip_err(e, "gradient reduction launch");
+    }
     const int64_t ntiles = (batch + 15) / 16;
     const int grid = (int)std::min<int64_t>(t->grid, (ntiles + kWavesPerBlock - 1) / kWavesPerBlock);
     for (const SweepOp& op : t->ops) {

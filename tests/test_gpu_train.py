@@ -95,7 +95,37 @@ def _mixed_spec(rng):
     ]}
 
 
-SPECS = {"readme": (_readme_spec, 5, 1), "cfg2": (_cfg2_spec, 5, 0), "mixed": (_mixed_spec, 6, 2)}
+def _wide_spec(rng):
+    """hidden 256 (the layer-wise path): a conditioned 8-d chain with MFMA-sized
+    outputs (4 transformed dims), a 3-Dense-hidden net and tanh."""
+    return {"kind": "chain", "layers": [
+        O.coupling_block(rng, O.coupling_axes_cut(8, 4, n=3), hidden=256, bias_scale=0.1, out_scale=0.1),
+        O.rnvp_layer(rng, O.coupling_axes(8, [2, 4, 6, 8, 1], n=3), n_sub=3, hidden=128, act="tanh",
+                     bias_scale=0.1, out_scale=0.2),
+        {"kind": "norm", "x_min": np.full(8, -3.0, np.float32), "x_max": np.full(8, 3.5, np.float32),
+         "alpha": 0.0, "beta": 1.0},
+    ]}
+
+
+def _cfg5_spec(rng):
+    """BASELINE configs[3]/[4] model: FlowChain(CouplingBlock, 8, 32; n = 8, hidden 256)."""
+    return {"kind": "chain", "layers": [
+        O.coupling_block(rng, O.coupling_axes_cut(32, n=8), hidden=256, bias_scale=0.1, out_scale=0.1)
+        for _ in range(8)]}
+
+
+SPECS = {"readme": (_readme_spec, 5, 1), "cfg2": (_cfg2_spec, 5, 0), "mixed": (_mixed_spec, 6, 2),
+         "wide": (_wide_spec, 8, 3), "cfg5": (_cfg5_spec, 32, 8)}
+
+
+@pytest.fixture(params=["fused", "layerwise"])
+def path(request, monkeypatch):
+    """Both training paths: the fused per-net kernel and the layer-wise GEMMs."""
+    if request.param == "layerwise":
+        monkeypatch.setenv("DF_TRAIN_LAYERWISE", "1")
+    else:
+        monkeypatch.delenv("DF_TRAIN_LAYERWISE", raising=False)
+    return request.param
 
 
 def _setup(name, seed=0):
@@ -124,7 +154,7 @@ def _gpu_grad(tr, x, th, cuda, n_total=None):
 
 
 @pytest.mark.parametrize("name,B", [("readme", 1000), ("cfg2", 3001), ("mixed", 777), ("readme", 1), ("cfg2", 17)])
-def test_gradient_parity(cuda, name, B):
+def test_gradient_parity(cuda, path, name, B):
     spec, chain, d, n = _setup(name)
     tr = HIPTrainer(chain.hip(), Adam())
     np.testing.assert_array_equal(tr.get_params(), trainables(chain))
@@ -141,8 +171,16 @@ def test_gradient_parity(cuda, name, B):
     assert worst <= 1.0, f"gradient violation ratio {worst}"
 
 
-def test_gradient_bitwise_reproducible(cuda):
-    spec, chain, d, n = _setup("cfg2")
+@pytest.mark.parametrize("name,B", [("wide", 700), ("wide", 5), ("cfg5", 300)])
+def test_gradient_parity_layerwise_wide(cuda, name, B):
+    """Conditioners beyond the fused kernel (hidden 128/256, 3 hidden Denses, MFMA
+    outputs): the layer-wise path is selected automatically."""
+    test_gradient_parity(cuda, "layerwise", name, B)
+
+
+@pytest.mark.parametrize("name", ["cfg2", "wide"])
+def test_gradient_bitwise_reproducible(cuda, path, name):
+    spec, chain, d, n = _setup(name)
     tr = HIPTrainer(chain.hip(), Adam())
     x, th = _inputs(d, n, 20000)
     g1, _ = _gpu_grad(tr, x, th, cuda)
@@ -150,7 +188,7 @@ def test_gradient_bitwise_reproducible(cuda):
     np.testing.assert_array_equal(g1, g2)
 
 
-def test_gradient_shards_sum(cuda):
+def test_gradient_shards_sum(cuda, path):
     """Data-parallel contract: shard gradients with n_total = global batch sum to the full gradient."""
     spec, chain, d, n = _setup("readme")
     tr = HIPTrainer(chain.hip(), Adam())
@@ -180,8 +218,8 @@ def _ulp_diff(a, b):
     return int(np.max(np.abs(ai - bi))) if ai.size else 0
 
 
-@pytest.mark.parametrize("name", ["readme", "mixed"])
-def test_adam_step_and_repack(cuda, name):
+@pytest.mark.parametrize("name", ["readme", "mixed", "wide"])
+def test_adam_step_and_repack(cuda, path, name):
     """Optimisers.update! on the device: the Float32 Adam formula to 1 ulp over
     two steps (βᵗ advances), and the chain's packed weights follow the update
     (forward / backward use the new parameters)."""
@@ -280,9 +318,6 @@ def test_train_matches_oracle_steps(cuda):
 
 def test_train_unsupported_structures(cuda):
     rng = np.random.default_rng(0)
-    wide = dfa.FlowChain.repeat(dfa.CouplingBlock, 1, 4, hidden_dim_s=128, hidden_dim_t=128, rng=rng)
-    with pytest.raises(dfa.UnsupportedError):
-        HIPTrainer(wide.hip(), Adam())
     sp = dfa.FlowChain(dfa.CouplingLayer(dfa.RNVPCouplingLayer, 4, 2, σ="softplus", rng=rng))
     with pytest.raises(dfa.UnsupportedError):
         HIPTrainer(sp.hip(), Adam())
