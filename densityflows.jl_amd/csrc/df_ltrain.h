@@ -30,8 +30,8 @@ enum : int { LEPI_ACT = 0, LEPI_COUPLE = 1, LEPI_DACT = 2, LEPI_XBAR = 3 };
 constexpr int kLChunkBytes = 32 * 1024;  // weight chunk (LDS, double-buffered)
 constexpr int kLTiles = 2;               // 16-sample tiles per wave per round
 constexpr int kLdwSamples = 32;          // samples per dW staging step
-constexpr int kLdwStride = kLdwSamples + 4;
-constexpr int kLdwMaxBlocks = 32;        // 16×16 output blocks per wave (registers)
+constexpr int kLdwBM = 8;                // per-wave output blocks (16×16): up to 8 row tiles
+constexpr int kLdwBN = 4;                //   × 4 column tiles (128 accumulator registers)
 
 struct LDenseArgs {
     const uint8_t* wfrag;   // fragments [kq][m][lane][4] of A (M = 16·MT rows)
@@ -70,6 +70,7 @@ struct LdwArgs {
     const float* xb;        // in [B][ldb] (rows = Dense inputs)
     int ldb, n_true;
     int mta, ntb;           // 16-row tiles of each operand
+    int wm, bm, bn;         // waves along M (8/wm along N); blocks per wave bm × bn
     float* partial;         // [workgroup][p_total]
     int64_t p_total;
     int w_off, b_off;       // trainables offsets (b_off -1: no bias)
@@ -82,5 +83,7 @@ hipError_t ldense_occupancy(int mt, int in_kind, int epi, size_t lds, int* block
 hipError_t set_ldense_lds_limit(size_t lds);
 hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st);
 size_t ldw_lds_bytes();
+// wave grid and per-wave blocks for a dW of mta × ntb tiles (host helper)
+bool ldw_shape(int mta, int ntb, int* wm, int* bm, int* bn);
 
 }  // namespace df

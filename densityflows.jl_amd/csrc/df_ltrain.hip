@@ -177,60 +177,99 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// dW = δ · inᵀ and db = Σ δ over this workgroup's contiguous sample range;
-// both operands staged transposed in LDS ([row][sample]); output 16×16 blocks
-// are dealt round-robin to the 8 waves and accumulated in registers.
+// dW = δ · inᵀ and db = Σ δ over this workgroup's contiguous sample range.
+// Both operands are staged sample-major in LDS (row stride ≡ 4 mod 8 floats:
+// the four lane groups of a half-wave hit disjoint banks), the next stage is
+// prefetched into registers while the current one is multiplied.  The 8 waves
+// form a wm × (8/wm) grid over the output tiles; each owns bm × bn 16×16
+// blocks in registers (k-step q of lane group g uses sample 16u + 4g + q).
 __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lsm[];
+    const int MA = 16 * a.mta, NB = 16 * a.ntb;
+    const int SA = MA + 4, SB = NB + 4;
     float* TA = lsm;
-    float* TB = lsm + 256 * kLdwStride;
+    float* TB = lsm + kLdwSamples * SA;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, j = lane & 15;
-    const int MA = 16 * a.mta, NB = 16 * a.ntb;
-    const int nblocks = a.mta * a.ntb;
+    const int wn = kWavesPerBlock / a.wm;
+    const int wi = wave % a.wm, wj = wave / a.wm;
+    const int m0 = wi * a.bm, n0 = wj * a.bn;  // first row / column tile of this wave
     const int64_t per = (a.batch + gridDim.x - 1) / gridDim.x;
     const int64_t s_begin = (int64_t)blockIdx.x * per;
     const int64_t s_end = (s_begin + per < a.batch) ? s_begin + per : a.batch;
+    (void)wn;
 
-    f32x4 acc[kLdwMaxBlocks / 1];
-    float db[kLdwMaxBlocks];
+    f32x4 acc[kLdwBM][kLdwBN];
+    float db[kLdwBM];
 #pragma unroll
-    for (int q = 0; q < kLdwMaxBlocks; ++q) {
-        acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-        db[q] = 0.f;
+    for (int im = 0; im < kLdwBM; ++im) {
+        db[im] = 0.f;
+#pragma unroll
+        for (int in = 0; in < kLdwBN; ++in) acc[im][in] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
+    // staging: thread e of a stage loads one f32x4 (sample e / (rows/4), row quad e % (rows/4))
+    const int qa = MA / 4, qb = NB / 4;
+    const int na = kLdwSamples * qa, nb = kLdwSamples * qb;
+    constexpr int kPre = (kLdwSamples * 256 / 4 + kBlockThreads - 1) / kBlockThreads;  // per operand
+    f32x4 pa[kPre], pb[kPre];
+    auto fetch = [&](int64_t s0) {
+#pragma unroll
+        for (int k = 0; k < kPre; ++k) {
+            const int e = tid + k * kBlockThreads;
+            pa[k] = pb[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (e < na) {
+                const int ss = e / qa, rq = e - ss * qa;
+                if (s0 + ss < s_end) pa[k] = *reinterpret_cast<const f32x4*>(a.da + (s0 + ss) * a.lda + 4 * rq);
+            }
+            if (e < nb) {
+                const int ss = e / qb, rq = e - ss * qb;
+                if (s0 + ss < s_end) pb[k] = *reinterpret_cast<const f32x4*>(a.xb + (s0 + ss) * a.ldb + 4 * rq);
+            }
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int k = 0; k < kPre; ++k) {
+            const int e = tid + k * kBlockThreads;
+            if (e < na) {
+                const int ss = e / qa, rq = e - ss * qa;
+                *reinterpret_cast<f32x4*>(TA + ss * SA + 4 * rq) = pa[k];
+            }
+            if (e < nb) {
+                const int ss = e / qb, rq = e - ss * qb;
+                *reinterpret_cast<f32x4*>(TB + ss * SB + 4 * rq) = pb[k];
+            }
+        }
+    };
+
+    if (s_begin < s_end) fetch(s_begin);
     for (int64_t s0 = s_begin; s0 < s_end; s0 += kLdwSamples) {
+        __syncthreads();  // previous stage consumed
+        stash();
         __syncthreads();
-        // stage [rows][32 samples] of both operands (zero beyond the range)
-        const int qa = MA / 4, qb = NB / 4;
-        for (int e = tid; e < kLdwSamples * qa; e += kBlockThreads) {
-            const int ss = e / qa, rq = e - ss * qa;
-            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (s0 + ss < s_end) v = *reinterpret_cast<const f32x4*>(a.da + (s0 + ss) * a.lda + 4 * rq);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) TA[(4 * rq + q) * kLdwStride + ss] = v[q];
-        }
-        for (int e = tid; e < kLdwSamples * qb; e += kBlockThreads) {
-            const int ss = e / qb, rq = e - ss * qb;
-            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (s0 + ss < s_end) v = *reinterpret_cast<const f32x4*>(a.xb + (s0 + ss) * a.ldb + 4 * rq);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) TB[(4 * rq + q) * kLdwStride + ss] = v[q];
-        }
-        __syncthreads();
+        if (s0 + kLdwSamples < s_end) fetch(s0 + kLdwSamples);
 #pragma unroll
         for (int u = 0; u < kLdwSamples / 16; ++u) {
+            const float* ta = TA + (16 * u + 4 * g) * SA + 16 * m0 + j;
+            const float* tb = TB + (16 * u + 4 * g) * SB + 16 * n0 + j;
+            float fb[kLdwBN][4];
 #pragma unroll
-            for (int q = 0; q < kLdwMaxBlocks; ++q) {
-                const int b = wave + kWavesPerBlock * q;
-                if (b < nblocks) {
-                    const int ma = b / a.ntb, nb = b - ma * a.ntb;
-                    const f32x4 fa = *reinterpret_cast<const f32x4*>(TA + (16 * ma + j) * kLdwStride + 16 * u + 4 * g);
-                    const f32x4 fb = *reinterpret_cast<const f32x4*>(TB + (16 * nb + j) * kLdwStride + 16 * u + 4 * g);
+            for (int in = 0; in < kLdwBN; ++in)
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) acc[q] = mfma4(fa[k], fb[k], acc[q]);
-                    if (nb == 0) db[q] += trn::hsum4(fa);
+                for (int q = 0; q < 4; ++q) fb[in][q] = (in < a.bn) ? tb[q * SB + 16 * in] : 0.f;
+#pragma unroll
+            for (int im = 0; im < kLdwBM; ++im) {
+                if (im < a.bm) {
+                    float fa[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) fa[q] = ta[q * SA + 16 * im];
+                    if (wj == 0) db[im] += (fa[0] + fa[1]) + (fa[2] + fa[3]);
+#pragma unroll
+                    for (int in = 0; in < kLdwBN; ++in)
+                        if (in < a.bn)
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) acc[im][in] = mfma4(fa[q], fb[in][q], acc[im][in]);
                 }
             }
         }
@@ -238,19 +277,22 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
 
     float* dst = a.partial + (int64_t)blockIdx.x * a.p_total;
 #pragma unroll
-    for (int q = 0; q < kLdwMaxBlocks; ++q) {
-        const int b = wave + kWavesPerBlock * q;
-        if (b < nblocks) {
-            const int ma = b / a.ntb, nb = b - ma * a.ntb;
+    for (int im = 0; im < kLdwBM; ++im) {
+        if (im >= a.bm || m0 + im >= a.mta) continue;
+        const int ma = m0 + im;
+#pragma unroll
+        for (int in = 0; in < kLdwBN; ++in) {
+            if (in >= a.bn || n0 + in >= a.ntb) continue;
+            const int nbk = n0 + in;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = 16 * ma + 4 * g + r, col = 16 * nb + j;
-                if (row < a.m_true && col < a.n_true) dst[a.w_off + row + (int64_t)a.m_true * col] = acc[q][r];
+                const int row = 16 * ma + 4 * g + r, col = 16 * nbk + j;
+                if (row < a.m_true && col < a.n_true) dst[a.w_off + row + (int64_t)a.m_true * col] = acc[im][in][r];
             }
-            if (nb == 0) {
-                const float v = uni::xgroup_sum(db[q]);
-                if (g == 0 && a.b_off >= 0 && 16 * ma + j < a.m_true) dst[a.b_off + 16 * ma + j] = v;
-            }
+        }
+        if (wj == 0) {
+            const float v = uni::xgroup_sum(db[im]);
+            if (g == 0 && a.b_off >= 0 && 16 * ma + j < a.m_true) dst[a.b_off + 16 * ma + j] = v;
         }
     }
 }
@@ -308,7 +350,24 @@ hipError_t set_ldense_lds_limit(size_t lds) {
                                (int)ldw_lds_bytes());
 }
 
-size_t ldw_lds_bytes() { return (size_t)2 * 256 * kLdwStride * 4; }
+size_t ldw_lds_bytes() { return (size_t)kLdwSamples * (256 + 4) * 4 * 2; }
+
+bool ldw_shape(int mta, int ntb, int* wm, int* bm, int* bn) {
+    int best = 1 << 30;
+    bool ok = false;
+    for (int w : {8, 4, 2, 1}) {
+        const int wn = kWavesPerBlock / w;
+        const int m = (mta + w - 1) / w, n = (ntb + wn - 1) / wn;
+        if (m <= kLdwBM && n <= kLdwBN && m * n < best) {
+            best = m * n;
+            *wm = w;
+            *bm = m;
+            *bn = n;
+            ok = true;
+        }
+    }
+    return ok;
+}
 
 hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st) {
     void* args[] = {const_cast<LdwArgs*>(&a)};

@@ -467,6 +467,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             w.w_off = D.w_off;
             w.b_off = D.b_off;
             w.batch = batch;
+            if (!ldw_shape(w.mta, w.ntb, &w.wm, &w.bm, &w.bn)) return set_err(DF_ERR_UNSUPPORTED, "dW tiling");
             e = launch_ldw(w, (unsigned)t->lgrid, st);
             if (e != hipSuccess) return hip_err(e, "dW kernel launch");
         }
