@@ -192,4 +192,52 @@ function forward!(c::HIPFlowChain, z::Array{Float32,N}, θ::Array{Float32,N}) wh
     return nothing
 end
 
+# ---- training: train! (src/Flows.jl:380-445) on the device ----------------------
+struct AdamDesc                  # df_adam
+    eta::Float32
+    beta1::Float32
+    beta2::Float32
+    epsilon::Float32
+end
+
+mutable struct HIPTrainer
+    handle::Ptr{Cvoid}
+    chain::HIPFlowChain
+    n_params::Int
+end
+
+"""Optimisers.setup(Adam(η, β, ϵ), model) on the device; the trainer owns the flat trainables."""
+function HIPTrainer(c::HIPFlowChain; eta=1f-3, beta=(0.9f0, 0.999f0), epsilon=1f-8)
+    t = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:df_train_create, LIB), Cint, (Ptr{Ptr{Cvoid}}, Ptr{Cvoid}, Ref{AdamDesc}),
+                t, c.handle, AdamDesc(eta, beta[1], beta[2], epsilon)), "df_train_create")
+    n = Ref{Int64}(0)
+    check(ccall((:df_train_num_params, LIB), Cint, (Ptr{Cvoid}, Ref{Int64}), t[], n), "df_train_num_params")
+    obj = HIPTrainer(t[], c, n[])
+    finalizer(x -> ccall((:df_train_destroy, LIB), Cint, (Ptr{Cvoid},), x.handle), obj)
+    return obj
+end
+
+"""One mini-batch step of train! (gradient of loss(backward(m, x, θ)) + Adam update)."""
+function train_step!(t::HIPTrainer, x::Array{Float32,N}, θ::Array{Float32,N}) where {N}
+    B = prod(size(x)[2:N])
+    dx, dθ = _dev(sizeof(x)), _dev(max(sizeof(θ), 1))
+    try
+        _h2d(dx, x); t.chain.n > 0 && _h2d(dθ, θ)
+        check(ccall((:df_train_step, LIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Cvoid}),
+                    t.handle, dx, t.chain.n > 0 ? dθ : C_NULL, B, C_NULL, C_NULL), "df_train_step")
+    finally
+        foreach(_free, (dx, dθ))
+    end
+    return nothing
+end
+
+"""Flux.trainables order: per coupling layer s_net then t_net, per Dense vec(weight) then bias."""
+function trainables(t::HIPTrainer)
+    p = Vector{Float32}(undef, t.n_params)
+    check(ccall((:df_train_get_params, LIB), Cint, (Ptr{Cvoid}, Ptr{Float32}, Int64), t.handle, p, t.n_params),
+          "df_train_get_params")
+    return p
+end
+
 end # module
