@@ -71,6 +71,24 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
 #pragma unroll
             for (int m = 0; m < MT; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+        // B operand of k-quad kq (rows 16kq + 4g + q of each tile's samples)
+        auto load_x = [&](int kq, f32x4 (&x)[T]) {
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                if constexpr (IN == LIN_BUF) {
+                    x[t] = valid[t] ? *reinterpret_cast<const f32x4*>(a.in + smp[t] * a.ld_in + 16 * kq + 4 * g)
+                                    : f32x4{0.f, 0.f, 0.f, 0.f};
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int f = 16 * kq + 4 * g + q;
+                        x[t][q] = (valid[t] && f < a.n_in) ? gather_feature(a, a.feat[f], smp[t]) : 0.f;
+                    }
+                }
+            }
+        };
+        f32x4 xn[T];
+        load_x(0, xn);  // prefetched one k-quad ahead
         for (int c = 0; c < nchunks; ++c, ++i) {
             const uint8_t* buf = smem;
             if (nchunks > 1) {
@@ -84,19 +102,13 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
             for (int kq = kq0; kq < kq1; ++kq) {
                 f32x4 x[T];
 #pragma unroll
-                for (int t = 0; t < T; ++t) {
-                    if constexpr (IN == LIN_BUF) {
-                        x[t] = valid[t] ? *reinterpret_cast<const f32x4*>(a.in + smp[t] * a.ld_in + 16 * kq + 4 * g)
-                                        : f32x4{0.f, 0.f, 0.f, 0.f};
-                    } else {
+                for (int t = 0; t < T; ++t) x[t] = xn[t];
+                if (kq + 1 < a.nkq) load_x(kq + 1, xn);
+                if constexpr (IN == LIN_GATHER) {
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const int f = 16 * kq + 4 * g + q;
-                            x[t][q] = (valid[t] && f < a.n_in) ? gather_feature(a, a.feat[f], smp[t]) : 0.f;
-                        }
+                    for (int t = 0; t < T; ++t)
                         if (a.xsave && valid[t])
                             *reinterpret_cast<f32x4*>(a.xsave + smp[t] * a.ld_x + 16 * kq + 4 * g) = x[t];
-                    }
                 }
                 const uint8_t* wb = buf + (kq - kq0) * MT * 1024 + lane * 16;
 #pragma unroll

@@ -255,7 +255,21 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
             if (L.kind == DF_LAYER_RNVP) total_bytes += net_bytes(L.s_net, L.n_dense_s);
             total_bytes += net_bytes(L.t_net, L.n_dense_t);
         }
-        Packer pk(P, total_bytes <= kSingleStageCap ? kSingleStageCap : kStageCap);
+        // Wide conditioners (>= 128 hidden) run one 16-sample tile per wave, so the
+        // stage-switch barrier is amortised over the MFMAs of one stage: give them
+        // the largest stages that still fit twice next to the state tile.
+        int cap = kStageCap;
+        if (P.ht >= 8 && !uniform_shape) {
+            int tab_ints = 0;
+            for (int li = 0; li < desc->n_layers; ++li)
+                if (desc->layers[li].kind != DF_LAYER_NORM)
+                    tab_ints += 4 * ((desc->layers[li].n_nn + 3) / 4) + desc->layers[li].n_af;
+            const int state = kWavesPerBlock * 16 * P.stride * 4;
+            const int room = (160 * 1024 - state - round_up(tab_ints * 4, 16) - 1024) / 2;
+            cap = std::max(kStageCap, std::min(kBigStageCap, room / kStageAlign * kStageAlign));
+        }
+        if (const char* e = std::getenv("DF_STAGE_KB")) cap = std::max(4, std::atoi(e)) * 1024;
+        Packer pk(P, total_bytes <= kSingleStageCap ? kSingleStageCap : cap);
         const int zero_slot = n + d;
         for (int li = 0; li < desc->n_layers; ++li) {
             const df_layer_desc& L = desc->layers[li];

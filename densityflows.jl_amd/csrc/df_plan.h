@@ -28,6 +28,7 @@ constexpr int kMaxAf = 32;           // transformed dims per coupling layer
 constexpr int kMaxLayers = 4096;
 constexpr int kStageCap = 24 * 1024;       // LDS weight stage buffer (double-buffered)
 constexpr int kSingleStageCap = 64 * 1024; // a whole chain this small lives in one stage
+constexpr int kBigStageCap = 64 * 1024;    // stages of wide (>= 128 hidden) generic-kernel chains
 constexpr int kStageAlign = 1024;          // one global->LDS DMA wave instruction (64 lanes x 16 B)
 constexpr int kMaxTableInts = 4096;  // 16 KiB of int32 tables in LDS
 constexpr int kMaxTilesPerWave = 8;          // 16-sample tiles per wave resident in LDS
