@@ -218,7 +218,7 @@ namespace df {
 namespace api {
 
 int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, float* xout, float* ldj, float* lp,
-        double* sum_out, int64_t batch, void* stream, float* snap) {
+        double* sum_out, int64_t batch, void* stream, float* snap, float* hsave, int hsave_w, int hsave_h) {
     if (!c) return set_err(DF_ERR_INVALID, "null chain");
     if (batch < 0) return set_err(DF_ERR_SHAPE, "negative batch size");
     const df::Plan& P = c->plan;
@@ -285,6 +285,9 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     // Distributions.mvnormal_c0: -(d * log2π + logdetcov)/2 in Float32, logdet(I) = 0
     a.c0 = -((float)P.d * (float)kLog2Pi + 0.f) / 2.f;
     a.snap = snap;
+    a.hsave = P.uniform ? nullptr : hsave;
+    a.hsave_w = hsave_w;
+    a.hsave_h = hsave_h;
 
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipError_t e = df::launch_chain(P.ht, mode, P.outv != 0, uniform_variant(P), a, (unsigned)grid,

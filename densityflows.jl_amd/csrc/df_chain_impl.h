@@ -303,7 +303,7 @@ __device__ __forceinline__ void dense_mfma(const ChainArgs& a, const DevDense& D
 template <int HT, int T, bool OUTV>
 __device__ __forceinline__ void eval_net(const ChainArgs& a, const DevLayer& L, int dense0, int ndense,
                                          Stager& sg, const Smem& sm, const int (&rowoff)[T],
-                                         NetRegs<HT, T, OUTV>& R) {
+                                         NetRegs<HT, T, OUTV>& R, float* hs = nullptr, int64_t gs = -1) {
     const int lane = threadIdx.x & 63;
     const int g = lane >> 4;
     const int32_t* feat = sm.tab + L.feat_tab;
@@ -359,6 +359,12 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const DevLayer& L, 
             for (int tt = 0; tt < T; ++tt)
 #pragma unroll
                 for (int m = 0; m < HT; ++m) R.h[tt][m] = R.acc[tt][m];
+            if (hs && gs >= 0) {  // training: keep H_k (post-activation), sample-major
+                float* dst = hs + ((int64_t)k * a.batch + gs) * a.hsave_w + 4 * g;
+#pragma unroll
+                for (int m = 0; m < HT; ++m)
+                    if (m < D.mt) *reinterpret_cast<f32x4*>(dst + 16 * m) = R.acc[0][m];
+            }
         }
     }
 }
@@ -548,16 +554,26 @@ chain_kernel(ChainArgs a) {
                     if (!rnvp) ldj_update(rowoff[0], 0.f, first_in_elem, last_in_elem);
                 }
             } else {
+                float* hs_t = nullptr;
+                float* hs_s = nullptr;
+                if (a.hsave) {
+                    hs_s = a.hsave + (int64_t)(2 * li) * a.hsave_h * a.batch * a.hsave_w;
+                    hs_t = hs_s + (int64_t)a.hsave_h * a.batch * a.hsave_w;
+                }
+                auto gs_of = [&](int tt) -> int64_t {
+                    const int smp = (wave * nt + tt) * 16 + j;
+                    return smp < nvalid ? s0 + smp : -1;
+                };
                 for (int tt = 0; tt < nt; ++tt) {
                     rowoff[0] = row_of(tt);
-                    eval_net<HT, T, OUTV>(a, L, L.t_dense0, L.t_ndense, sg, sm, rowoff, R);
+                    eval_net<HT, T, OUTV>(a, L, L.t_dense0, L.t_ndense, sg, sm, rowoff, R, hs_t, gs_of(tt));
                     couple_phase<HT, T, OUTV, PH_T_BWD>(R, L, sm, rowoff, ssum);
                     if (!rnvp) ldj_update(rowoff[0], 0.f, first_in_elem, last_in_elem);
                 }
                 if (rnvp) {
                     for (int tt = 0; tt < nt; ++tt) {
                         rowoff[0] = row_of(tt);
-                        eval_net<HT, T, OUTV>(a, L, L.s_dense0, L.s_ndense, sg, sm, rowoff, R);
+                        eval_net<HT, T, OUTV>(a, L, L.s_dense0, L.s_ndense, sg, sm, rowoff, R, hs_s, gs_of(tt));
                         couple_phase<HT, T, OUTV, PH_S_BWD>(R, L, sm, rowoff, ssum);
                         ldj_update(rowoff[0], -ssum[0], first_in_elem, last_in_elem);  // ln_det_jac = -Σ s
                     }

@@ -74,7 +74,8 @@ constexpr double kLog2Pi = 1.8378770664093453;  // log(2π)
 // Launch one fused chain pass.  flow: θ normalised with the handle's bounds;
 // snap (inverse modes, specialised kernel): every layer's output kept.
 int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, float* xout, float* ldj, float* lp,
-        double* sum_out, int64_t batch, void* stream, float* snap = nullptr);
+        double* sum_out, int64_t batch, void* stream, float* snap = nullptr, float* hsave = nullptr,
+        int hsave_w = 0, int hsave_h = 0);
 
 }  // namespace api
 }  // namespace df

@@ -43,7 +43,10 @@ struct ChainArgs {
     int n_sched_fwd;
     int n_sched_bwd;
     float c0;            // -(d·log2π)/2
-    float* snap;         // inverse modes, specialised kernel: state after each layer, [layer][sample][d]
+    float* snap;         // inverse modes: state after each layer, [layer][sample][d]
+    float* hsave;        // inverse modes, generic kernel: hidden activations of every net,
+                         // [(layer·2 + net)·hsave_h + k][sample][hsave_w] (training, layer-wise path)
+    int hsave_w, hsave_h;
 };
 
 // Per-variant entry points (explicitly instantiated in df_kernels_ht*.hip).

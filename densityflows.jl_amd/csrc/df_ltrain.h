@@ -82,6 +82,8 @@ hipError_t launch_ldense(int mt, int in_kind, int epi, const LDenseArgs& a, unsi
 hipError_t ldense_occupancy(int mt, int in_kind, int epi, size_t lds, int* blocks);
 hipError_t set_ldense_lds_limit(size_t lds);
 hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st);
+// conditioner input vcat(θ, u)[axis_nn] → xsave [B][ld_x] (rows >= n_in zero), for dW0
+hipError_t launch_gather_features(const LDenseArgs& a, int rows, hipStream_t st);
 size_t ldw_lds_bytes();
 // wave grid and per-wave blocks for a dW of mta × ntb tiles (host helper)
 bool ldw_shape(int mta, int ntb, int* wm, int* bm, int* bn);

@@ -309,6 +309,14 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
     }
 }
 
+__global__ void gather_features_kernel(LDenseArgs a, int rows) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.batch * rows) return;
+    const int64_t s = i / rows;
+    const int f = (int)(i - s * rows);
+    a.xsave[s * a.ld_x + f] = (f < a.n_in) ? gather_feature(a, a.feat[f], s) : 0.f;
+}
+
 template <int MT>
 void* ldense_ptr_mt(int in_kind, int epi) {
     if (in_kind == LIN_GATHER) return reinterpret_cast<void*>(&ldense_kernel<MT, LIN_GATHER, LEPI_ACT>);
@@ -360,6 +368,13 @@ hipError_t set_ldense_lds_limit(size_t lds) {
     }
     return hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)ldw_lds_bytes());
+}
+
+hipError_t launch_gather_features(const LDenseArgs& a, int rows, hipStream_t st) {
+    const int64_t n = a.batch * rows;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_features_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, rows);
+    return hipGetLastError();
 }
 
 size_t ldw_lds_bytes() { return (size_t)kLdwSamples * (256 + 4) * 4 * 2; }

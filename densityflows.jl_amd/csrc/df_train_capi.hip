@@ -100,6 +100,10 @@ struct df_train {
     std::vector<float*> d_lh, d_ld; // H_k and δ_k buffers [cap][lwidth]
     float* d_ly = nullptr;           // ȳ  [cap][lwidth]
     float* d_lx = nullptr;           // gathered conditioner input [cap][lwidth]
+    // hidden activations kept by the inverse pass (generic kernel): the sweep then
+    // skips the forward recompute.  [(layer·2 + net)·lmax_h + k][B][lwidth]
+    float* d_hsave = nullptr;
+    bool hsave_on = false;
 };
 
 namespace {
@@ -107,7 +111,7 @@ namespace {
 void free_all(df_train* t) {
     void* ptrs[] = {t->d_params, t->d_m,    t->d_v,    t->d_grad, t->d_partial, t->d_tblob, t->d_pdst,
                     t->d_psrc,   t->d_tdst, t->d_tsrc, t->d_snap, t->d_zbar,    t->d_ebuf,  t->d_lpsum,
-                    t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_ly,   t->d_lx};
+                    t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_ly,   t->d_lx,      t->d_hsave};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (float* p : t->d_lh)
@@ -316,7 +320,7 @@ int ensure_capacity(df_train* t, int64_t batch) {
         }
     t->cap = 0;
     const int64_t cap = std::max<int64_t>(batch, 1024);
-    for (float** p : {&t->d_ly, &t->d_lx})
+    for (float** p : {&t->d_ly, &t->d_lx, &t->d_hsave})
         if (*p) {
             (void)hipFree(*p);
             *p = nullptr;
@@ -336,6 +340,17 @@ int ensure_capacity(df_train* t, int64_t batch) {
         if (hipMalloc(reinterpret_cast<void**>(&t->d_ly), row) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&t->d_lx), row) != hipSuccess)
             return set_err(DF_ERR_NOMEM, "hipMalloc failed (training activations)");
+        // keep the inverse pass's hidden activations when the chain runs on the generic
+        // kernel and they fit (else the sweep recomputes them)
+        t->hsave_on = false;
+        if (!P.uniform && !(std::getenv("DF_TRAIN_RECOMPUTE") && std::getenv("DF_TRAIN_RECOMPUTE")[0] == '1')) {
+            const size_t hbytes = row * (size_t)P.n_layers * 2 * t->lmax_h;
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && hbytes < free_b / 2 &&
+                hipMalloc(reinterpret_cast<void**>(&t->d_hsave), hbytes) == hipSuccess)
+                t->hsave_on = true;
+            (void)hipGetLastError();
+        }
         for (int k = 0; k <= t->lmax_h; ++k) {
             float *h = nullptr, *dl = nullptr;
             if (hipMalloc(reinterpret_cast<void**>(&h), row) != hipSuccess ||
@@ -416,17 +431,29 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         b.d = P.d;
         b.n = P.n;
         b.ld_in = b.ld_out = b.ld_h = b.ld_x = W;
-        // forward recompute: H_k = σ(W_k · in + b_k), then the output Dense + coupling pullback → ȳ
+        // H_k: kept by the inverse pass, or recomputed here
+        const int net_slot = 2 * op.layer + (op.phase == TR_PHASE_T ? 1 : 0);
+        auto H = [&](int k) -> float* {
+            return t->hsave_on ? t->d_hsave + ((int64_t)net_slot * t->lmax_h + k) * batch * W : t->d_lh[k];
+        };
+        // forward (recompute): H_k = σ(W_k · in + b_k), then the output Dense + coupling pullback → ȳ
         for (int k = 0; k < nd; ++k) {
             LDenseArgs a = b;
             a.act = N.dn[k].act;
+            if (k + 1 < nd && t->hsave_on) {
+                if (k == 0) {
+                    a.xsave = t->d_lx;
+                    e = e == hipSuccess ? launch_gather_features(a, 16 * N.dn[0].bwd.mt, st) : e;
+                }
+                continue;
+            }
             if (k == 0) {
                 a.xsave = t->d_lx;
             } else {
-                a.in = t->d_lh[k - 1];
+                a.in = H(k - 1);
             }
             if (k + 1 < nd) {
-                a.out = t->d_lh[k];
+                a.out = H(k);
                 dense(N.dn[k].fwd, k == 0 ? LIN_GATHER : LIN_BUF, LEPI_ACT, a);
             } else {
                 a.out = t->d_ly;
@@ -438,7 +465,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         for (int k = nd - 1; k >= 1; --k) {
             LDenseArgs a = b;
             a.in = gcur;
-            a.hprev = t->d_lh[k - 1];
+            a.hprev = H(k - 1);
             a.dact = N.dn[k - 1].act;
             a.out = t->d_ld[k - 1];
             dense(N.dn[k].bwd, LIN_BUF, LEPI_DACT, a);
@@ -458,7 +485,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             w.lda = W;
             w.m_true = D.out_dim;
             w.mta = D.fwd.mt;
-            w.xb = (k == 0) ? t->d_lx : t->d_lh[k - 1];
+            w.xb = (k == 0) ? t->d_lx : H(k - 1);
             w.ldb = W;
             w.n_true = D.in_dim;
             w.ntb = D.bwd.mt;
@@ -622,7 +649,7 @@ int df_train_gradient(df_train* t, const float* x, const float* theta_raw, int64
 
     // 1. inverse pass keeping every layer's output (U[li] = snap[li], U[0] = z)
     rc = run(c, MODE_LOGPDF, flow, x, theta_raw, nullptr, nullptr, nullptr, logpdf_sum ? logpdf_sum : t->d_lpsum,
-             batch, stream, t->d_snap);
+             batch, stream, t->d_snap, t->hsave_on ? t->d_hsave : nullptr, t->lwidth, t->lmax_h);
     if (rc != DF_OK) return rc;
     const int64_t bd = batch * P.d;
     // 2. z̄ = z / N

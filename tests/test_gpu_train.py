@@ -171,10 +171,16 @@ def test_gradient_parity(cuda, path, name, B):
     assert worst <= 1.0, f"gradient violation ratio {worst}"
 
 
+@pytest.mark.parametrize("recompute", [False, True])
 @pytest.mark.parametrize("name,B", [("wide", 700), ("wide", 5), ("cfg5", 300)])
-def test_gradient_parity_layerwise_wide(cuda, name, B):
+def test_gradient_parity_layerwise_wide(cuda, monkeypatch, name, B, recompute):
     """Conditioners beyond the fused kernel (hidden 128/256, 3 hidden Denses, MFMA
-    outputs): the layer-wise path is selected automatically."""
+    outputs): the layer-wise path is selected automatically.  By default the
+    inverse pass keeps the hidden activations; DF_TRAIN_RECOMPUTE=1 recomputes them."""
+    if recompute:
+        monkeypatch.setenv("DF_TRAIN_RECOMPUTE", "1")
+    else:
+        monkeypatch.delenv("DF_TRAIN_RECOMPUTE", raising=False)
     test_gradient_parity(cuda, "layerwise", name, B)
 
 
