@@ -238,6 +238,36 @@ __device__ __forceinline__ void dense_mfma(const ChainArgs& a, const DevDense& D
                                 acc[tt][m0 + mm] = mfma4(w[cb][mm][r], h[tt][kq][r], acc[tt][m0 + mm]);
                 }
             }
+        } else if (D.mt == HT) {
+            // full-M hidden Dense streamed in K-chunks (wide nets: one chunk per stage):
+            // a uniform scalar guard per k-quad, no per-tile guards, MB interleaved
+            // accumulators, fragments of the next m-group read ahead.
+            constexpr int MB = HT < 4 ? HT : 4;
+            const int kb = C.kq_begin, ke = C.kq_end;
+#pragma unroll
+            for (int kq = 0; kq < HT; ++kq) {
+                if (kq >= kb && kq < ke) {
+                    const uint8_t* bq = base + (kq - kb) * HT * 1024;
+                    f32x4 w[2][MB];
+#pragma unroll
+                    for (int mm = 0; mm < MB; ++mm) w[0][mm] = lds4(bq + mm * 1024);
+#pragma unroll
+                    for (int m0 = 0; m0 < HT; m0 += MB) {
+                        const int cb = (m0 / MB) & 1;
+                        if (m0 + MB < HT) {
+#pragma unroll
+                            for (int mm = 0; mm < MB; ++mm) w[cb ^ 1][mm] = lds4(bq + (m0 + MB + mm) * 1024);
+                        }
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+#pragma unroll
+                            for (int mm = 0; mm < MB; ++mm)
+#pragma unroll
+                                for (int tt = 0; tt < T; ++tt)
+                                    acc[tt][m0 + mm] = mfma4(w[cb][mm][r], h[tt][kq][r], acc[tt][m0 + mm]);
+                    }
+                }
+            }
         } else {
 #pragma unroll
             for (int kq = 0; kq < HT; ++kq) {
