@@ -188,6 +188,26 @@ __device__ __forceinline__ void dense_mfma(const ChainArgs& a, const DevDense& D
                         }
                     }
                     const uint8_t* bq = base + (kq - C.kq_begin) * D.mt * 1024;
+                    if (HT >= 8 && D.mt == HT) {
+                        // full-M first Dense of a wide net: no per-tile guards, 4 chains
+                        constexpr int MB = HT < 4 ? HT : 4;
+                        const int rmax = D.ks - 4 * kq;  // k-steps of this k-quad that carry features
+#pragma unroll
+                        for (int m0 = 0; m0 < HT; m0 += MB) {
+                            f32x4 w[MB];
+#pragma unroll
+                            for (int mm = 0; mm < MB; ++mm) w[mm] = lds4(bq + (m0 + mm) * 1024);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                if (r < rmax)
+#pragma unroll
+                                    for (int mm = 0; mm < MB; ++mm)
+#pragma unroll
+                                        for (int tt = 0; tt < T; ++tt)
+                                            acc[tt][m0 + mm] = mfma4(w[mm][r], xin[tt][r], acc[tt][m0 + mm]);
+                        }
+                        continue;
+                    }
 #pragma unroll
                     for (int m0 = 0; m0 < HT; m0 += MG) {
                         if (m0 < D.mt) {
@@ -236,6 +256,31 @@ __device__ __forceinline__ void dense_mfma(const ChainArgs& a, const DevDense& D
 #pragma unroll
                             for (int tt = 0; tt < T; ++tt)
                                 acc[tt][m0 + mm] = mfma4(w[cb][mm][r], h[tt][kq][r], acc[tt][m0 + mm]);
+                }
+            }
+        } else if (HT >= 8 && D.mt <= 2) {
+            // narrow output Dense of a wide net (<= 32 outputs): two tiles at most
+            const int kb = C.kq_begin, ke = C.kq_end;
+#pragma unroll
+            for (int kq = 0; kq < HT; ++kq) {
+                if (kq >= kb && kq < ke) {
+                    const uint8_t* bq = base + (kq - kb) * D.mt * 1024;
+                    const f32x4 w0 = lds4(bq);
+                    if (D.mt == 2) {
+                        const f32x4 w1 = lds4(bq + 1024);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+#pragma unroll
+                            for (int tt = 0; tt < T; ++tt) {
+                                acc[tt][0] = mfma4(w0[r], h[tt][kq][r], acc[tt][0]);
+                                acc[tt][1] = mfma4(w1[r], h[tt][kq][r], acc[tt][1]);
+                            }
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+#pragma unroll
+                            for (int tt = 0; tt < T; ++tt) acc[tt][0] = mfma4(w0[r], h[tt][kq][r], acc[tt][0]);
+                    }
                 }
             }
         } else if (D.mt == HT) {

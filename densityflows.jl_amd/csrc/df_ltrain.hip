@@ -383,6 +383,7 @@ bool ldw_shape(int mta, int ntb, int* wm, int* bm, int* bn) {
     int best = 1 << 30;
     bool ok = false;
     for (int w : {8, 4, 2, 1}) {
+        if (w > kWavesPerBlock) continue;
         const int wn = kWavesPerBlock / w;
         const int m = (mta + w - 1) / w, n = (ntb + wn - 1) / wn;
         if (m <= kLdwBM && n <= kLdwBN && m * n < best) {

@@ -20,7 +20,13 @@
 namespace df {
 
 constexpr int kWave = 64;
-constexpr int kBlockThreads = 512;   // 8 waves per workgroup
+#ifndef DF_BLOCK_WAVES
+#define DF_BLOCK_WAVES 8
+#endif
+#ifndef DF_LDS_TARGET_KB
+#define DF_LDS_TARGET_KB 80
+#endif
+constexpr int kBlockThreads = 64 * DF_BLOCK_WAVES;  // 8 waves per workgroup
 constexpr int kWavesPerBlock = kBlockThreads / kWave;
 constexpr int kMaxState = 64;        // n + d (conditioner input <= 64 features)
 constexpr int kMaxHidden = 256;      // widest Dense (16 MFMA row tiles)
@@ -36,7 +42,7 @@ constexpr int kMaxTilesPerWave = 8;          // 16-sample tiles per wave residen
 #define DF_UNI_TT 1
 #endif
 constexpr int kUniformTileGroup = DF_UNI_TT;  // tiles the specialised kernel evaluates together
-constexpr int kLdsPerBlockTarget = 80 * 1024; // two workgroups per CU
+constexpr int kLdsPerBlockTarget = DF_LDS_TARGET_KB * 1024; // two workgroups per CU
 
 enum : int32_t { IN_STATE = 0, IN_HIDDEN = 1 };
 
