@@ -45,7 +45,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace impl {
 
-__device__ __forceinline__ float relu(float x) { return (x > 0.f) ? x : ((x == x) ? 0.f : x); }
+// relu = max(0, x) as ONE v_max_i32 on the bit pattern: non-negative floats order
+// like their integer images, negatives and -0 map to +0, and NaNs with the sign
+// bit clear (every NaN the GPU produces) propagate as in Julia.
+__device__ __forceinline__ float relu(float x) {
+    return __int_as_float(__builtin_elementwise_max(__float_as_int(x), 0));
+}
 
 __device__ __noinline__ float act_fn(int act, float x) {
     switch (act) {
