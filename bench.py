@@ -135,7 +135,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=1 << 20, help="samples per GPU")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="samples per GPU (default: the config's: 2^20 for cfg1/cfg2, 2^18 for cfg4 = configs[3] "
+                         "and the per-GPU share of configs[4])")
     ap.add_argument("--mode", choices=["forward", "nll", "train"], default="forward")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg2",
                     help="cfg2 is the headline (BASELINE configs[1]); cfg1/cfg4 are secondary measurements")
@@ -171,7 +173,7 @@ def main():
     chain = build_chain(args.config)
     hc = chain.hip(device=gpu, n_hint=n)
     info = hc.info
-    B = args.batch
+    B = args.batch if args.batch is not None else (1 << 18 if args.config == "cfg4" else 1 << 20)
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     zbuf = torch.randn(B * d, device=dev, generator=gen)      # Julia (d, B) column-major
     thbuf = torch.rand(B * n, device=dev, generator=gen) if n > 0 else None
