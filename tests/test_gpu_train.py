@@ -358,3 +358,41 @@ def test_data_parallel_train_matches_single(cuda, tmp_path):
     # move near-zero-gradient coordinates by O(η) over the run
     assert np.max(np.abs(dp["params"] - p1)) <= 2e-3
     assert np.mean(np.abs(dp["params"] - p1)) <= 2e-5
+
+
+def _nice_only_spec(rng):
+    layers = []
+    for m in ([1, 2], [3, 4], [2, 4]):
+        L = O.rnvp_layer(rng, O.coupling_axes(4, m, n=1), hidden=32, bias_scale=0.1)
+        L["kind"] = "nice"
+        del L["s_net"]
+        layers.append(L)
+    norm = {"kind": "norm", "x_min": np.full(4, -2.5, np.float32), "x_max": np.full(4, 2.0, np.float32),
+            "alpha": -1.0, "beta": 1.0}
+    return {"kind": "chain", "layers": [dict(norm), *layers, dict(norm)]}
+
+
+def _nobias_spec(rng):
+    blk = O.coupling_block(rng, O.coupling_axes_cut(6, 3, n=0), hidden=64, bias_scale=0.1, out_scale=0.2)
+    for L in (blk["layer_1"], blk["layer_2"]):
+        for net in ("s_net", "t_net"):
+            L[net][0]["b"] = None          # Dense(...; bias=false)
+            L[net][-1]["b"] = None
+    return {"kind": "chain", "layers": [blk]}
+
+
+def _d2_spec(rng):
+    return {"kind": "chain", "layers": [
+        O.coupling_block(rng, O.coupling_axes_cut(2, 1, n=0), hidden=16, bias_scale=0.1, out_scale=0.5)
+        for _ in range(3)]}
+
+
+SPECS.update({"nice_only": (_nice_only_spec, 4, 1), "nobias": (_nobias_spec, 6, 0), "d2": (_d2_spec, 2, 0)})
+
+
+@pytest.mark.parametrize("name,B", [("nice_only", 15), ("nice_only", 16), ("nobias", 17), ("nobias", 4097),
+                                    ("d2", 33), ("cfg2", 4096)])
+def test_gradient_parity_edge_cases(cuda, path, name, B):
+    """NICE-only chains between NormalizationLayers, Denses without bias,
+    unconditional 2-d chains, and batches around the 16-sample tile."""
+    test_gradient_parity(cuda, path, name, B)
