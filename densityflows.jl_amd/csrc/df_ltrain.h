@@ -25,7 +25,7 @@
 namespace df {
 
 enum : int { LIN_BUF = 0, LIN_GATHER = 1 };
-enum : int { LEPI_ACT = 0, LEPI_COUPLE = 1, LEPI_DACT = 2, LEPI_XBAR = 3 };
+enum : int { LEPI_ACT = 0, LEPI_COUPLE = 1, LEPI_DACT = 2, LEPI_XBAR = 3, LEPI_DACT_XBAR = 4 };
 
 constexpr int kLChunkBytes = 32 * 1024;  // weight chunk (LDS, double-buffered)
 constexpr int kLTiles = 2;               // 16-sample tiles per wave per round
@@ -62,6 +62,13 @@ struct LDenseArgs {
     float inv_n;
     int64_t batch;
     int d, n;
+    // LEPI_DACT_XBAR: x̄ = W0ᵀ δ0 right after δ0 (fragments resident in LDS)
+    const uint8_t* w0t;
+    int w0t_mt, w0t_nkq;
+    // couple_bwd_kernel: second product W_outᵀ ȳ (fragments [kq][m][lane][4], m < 16·HT rows)
+    const uint8_t* w2frag;
+    int nkq2;
+    float* out2;            // δ of the last hidden Dense [B][ld_out]
 };
 
 struct LdwArgs {
@@ -82,6 +89,10 @@ hipError_t launch_ldense(int mt, int in_kind, int epi, const LDenseArgs& a, unsi
 hipError_t ldense_occupancy(int mt, int in_kind, int epi, size_t lds, int* blocks);
 hipError_t set_ldense_lds_limit(size_t lds);
 hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st);
+// Output Dense + coupling pullback → ȳ, then δ = (W_outᵀ ȳ) ⊙ σ'(H) in one pass over H
+// (ht: 16-row tiles of H, mto: output tiles <= 2).  LDS: both fragment sets.
+hipError_t launch_couple_bwd(int ht, int mto, const LDenseArgs& a, unsigned grid, size_t lds, hipStream_t st);
+hipError_t set_couple_bwd_lds_limit(size_t lds);
 // conditioner input vcat(θ, u)[axis_nn] → xsave [B][ld_x] (rows >= n_in zero), for dW0
 hipError_t launch_gather_features(const LDenseArgs& a, int rows, hipStream_t st);
 size_t ldw_lds_bytes();

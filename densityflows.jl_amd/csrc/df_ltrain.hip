@@ -49,8 +49,15 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
                                              (__attribute__((address_space(3))) void*)(dst + (q << 10)), 16, 0,
                                              0);
     };
+    // after the chunk buffer(s): two full chunks, or the single (possibly short) one
+    uint8_t* w0t_lds = smem + (nchunks > 1 ? 2 * chunk_bytes : a.nkq * MT * 1024);
+    if constexpr (EPI == LEPI_DACT_XBAR) {  // W0ᵀ fragments stay resident for the x̄ product
+        const int n16 = a.w0t_mt * a.w0t_nkq * 64;
+        const f32x4* src = reinterpret_cast<const f32x4*>(a.w0t);
+        for (int q = threadIdx.x; q < n16; q += kBlockThreads) reinterpret_cast<f32x4*>(w0t_lds)[q] = src[q];
+    }
     dma(0, smem);
-    if (nchunks == 1) {
+    if (nchunks == 1 || EPI == LEPI_DACT_XBAR) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -125,8 +132,10 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
         // ---- epilogue: rows 16m + 4g + q of sample smp[t] ----
 #pragma unroll
         for (int t = 0; t < T; ++t) {
-            if (!valid[t]) continue;
-            const int64_t s = smp[t];
+            // LEPI_DACT_XBAR runs an MFMA in its epilogue: keep EXEC full (MFMA operands
+            // cross lanes), guard only the memory accesses
+            if (EPI != LEPI_DACT_XBAR && !valid[t]) continue;
+            const int64_t s = valid[t] ? smp[t] : 0;
 #pragma unroll
             for (int m = 0; m < MT; ++m) {
                 const int row0 = 16 * m + 4 * g;
@@ -163,8 +172,9 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
                         }
                     }
                     *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = dy;
-                } else if constexpr (EPI == LEPI_DACT) {
-                    const f32x4 h = *reinterpret_cast<const f32x4*>(a.hprev + s * a.ld_h + row0);
+                } else if constexpr (EPI == LEPI_DACT || EPI == LEPI_DACT_XBAR) {
+                    const f32x4 h = valid[t] ? *reinterpret_cast<const f32x4*>(a.hprev + s * a.ld_h + row0)
+                                             : f32x4{0.f, 0.f, 0.f, 0.f};
                     if (a.dact == DF_ACT_RELU) {
 #pragma unroll
                         for (int q = 0; q < 4; ++q) v[q] = (h[q] > 0.f) ? v[q] : 0.f;
@@ -172,7 +182,9 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
 #pragma unroll
                         for (int q = 0; q < 4; ++q) v[q] = v[q] * trn::act_grad(a.dact, h[q]);
                     }
-                    *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = v;
+                    if (!valid[t]) v = f32x4{0.f, 0.f, 0.f, 0.f};
+                    else *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = v;
+                    if constexpr (EPI == LEPI_DACT_XBAR) acc[t][m] = v;  // δ0 → B operand of W0ᵀ
                 } else {  // LEPI_XBAR: conditioner-input gradient into z̄ of identity dims
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -184,10 +196,166 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
                     }
                 }
             }
+            if constexpr (EPI == LEPI_DACT_XBAR) {
+                // x̄ = W0ᵀ δ0 (rows = conditioner features, <= 4 tiles) → z̄ of identity dims
+                f32x4 xb[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) xb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kq = 0; kq < MT; ++kq) {
+                    if (kq < a.w0t_nkq) {
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) {
+                            if (m < a.w0t_mt) {
+                                const f32x4 w = lds4(w0t_lds + (kq * a.w0t_mt + m) * 1024 + lane * 16);
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) xb[m] = mfma4(w[q], acc[t][kq][q], xb[m]);
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    if (m < a.w0t_mt) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const int f = 16 * m + 4 * g + q;
+                            if (valid[t] && f < a.n_in) {
+                                const int slot = a.feat[f];
+                                if (slot >= a.n && slot < a.n + a.d) a.zbar[s * a.d + (slot - a.n)] += xb[m][q];
+                            }
+                        }
+                    }
+                }
+            }
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
+
+// Output Dense + coupling pullback, then δ = (W_outᵀ ȳ) ⊙ σ'(H): H (the last hidden
+// activation, kept by the inverse pass) is read once and serves as the B operand of
+// the first product and as the σ' argument of the second; ȳ stays in registers as
+// the B operand of the second (accumulator layout = B layout).  One 16-sample tile
+// per wave per round; both fragment sets resident in LDS.
+template <int HT, int MTO>
+__global__ void __launch_bounds__(kBlockThreads, 1) couple_bwd_kernel(LDenseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* wo = smem;                         // W_out: [kq < HT][m < MTO]
+    uint8_t* wt = smem + HT * MTO * 1024;       // W_outᵀ: [kq < MTO][m < HT]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, j = lane & 15;
+    {
+        const int n1 = a.nkq * MTO * 64, n2 = a.nkq2 * HT * 64;
+        for (int q = tid; q < n1; q += kBlockThreads)
+            reinterpret_cast<f32x4*>(wo)[q] = reinterpret_cast<const f32x4*>(a.wfrag)[q];
+        for (int q = tid; q < n2; q += kBlockThreads)
+            reinterpret_cast<f32x4*>(wt)[q] = reinterpret_cast<const f32x4*>(a.w2frag)[q];
+    }
+    __syncthreads();
+    const int64_t ntiles = (a.batch + 15) / 16;
+    const bool sph = (a.phase == TR_PHASE_S);
+    const bool rnvp = (a.kind == DF_LAYER_RNVP);
+    for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wave; tile < ntiles;
+         tile += (int64_t)gridDim.x * kWavesPerBlock) {
+        const int64_t s = tile * 16 + j;
+        const bool valid = s < a.batch;
+        f32x4 h[HT];
+#pragma unroll
+        for (int kq = 0; kq < HT; ++kq)
+            h[kq] = (valid && kq < a.nkq) ? *reinterpret_cast<const f32x4*>(a.in + s * a.ld_in + 16 * kq + 4 * g)
+                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 y[MTO];
+#pragma unroll
+        for (int m = 0; m < MTO; ++m) y[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kq = 0; kq < HT; ++kq) {
+            if (kq < a.nkq) {
+#pragma unroll
+                for (int m = 0; m < MTO; ++m) {
+                    const f32x4 w = lds4(wo + (kq * MTO + m) * 1024 + lane * 16);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) y[m] = mfma4(w[q], h[kq][q], y[m]);
+                }
+            }
+        }
+        // σo(W_out h .+ b), then the coupling pullback (rrule(RNVP_backward) RNVP.jl:133-139)
+        f32x4 dy[MTO];
+#pragma unroll
+        for (int m = 0; m < MTO; ++m) {
+            const int row0 = 16 * m + 4 * g;
+            f32x4 v = y[m];
+            if (a.bias) v = v + *reinterpret_cast<const f32x4*>(a.bias + row0);
+            if (a.act != DF_ACT_IDENTITY)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = impl::act_fn(a.act, v[q]);
+            dy[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = row0 + q;
+                if (valid && row < a.n_af) {
+                    const int dim = a.af[row] - a.n;
+                    const float zb = a.zbar[s * a.d + dim];
+                    float dq;
+                    if (sph) {
+                        a.ebuf[s * 32 + row] = expf(-v[q]);
+                        dq = -zb * a.u_out[s * a.d + dim] + a.inv_n;  // s̄ = -z̄_af·z_af - j̄
+                    } else {
+                        const float e = rnvp ? a.ebuf[s * 32 + row] : 1.f;
+                        dq = -zb * e;                                   // t̄ = -z̄_af·exp(-s)
+                        if (rnvp) a.zbar[s * a.d + dim] = zb * e;       // ū_af = z̄_af·exp(-s)
+                    }
+                    if (a.act != DF_ACT_IDENTITY) dq = dq * trn::act_grad(a.act, v[q]);
+                    dy[m][q] = dq;
+                }
+            }
+            if (valid) *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = dy[m];
+        }
+        // δ = (W_outᵀ ȳ) ⊙ σ'(h)
+        f32x4 acc[HT];
+#pragma unroll
+        for (int m = 0; m < HT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kq = 0; kq < MTO; ++kq) {
+            if (kq < a.nkq2) {
+#pragma unroll
+                for (int m = 0; m < HT; ++m) {
+                    const f32x4 w = lds4(wt + (kq * HT + m) * 1024 + lane * 16);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[m] = mfma4(w[q], dy[kq][q], acc[m]);
+                }
+            }
+        }
+        if (valid) {
+#pragma unroll
+            for (int m = 0; m < HT; ++m) {
+                f32x4 v = acc[m];
+                if (a.dact == DF_ACT_RELU) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] = (h[m][q] > 0.f) ? v[q] : 0.f;
+                } else if (a.dact != DF_ACT_IDENTITY) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) v[q] = v[q] * trn::act_grad(a.dact, h[m][q]);
+                }
+                *reinterpret_cast<f32x4*>(a.out2 + s * a.ld_out + 16 * m + 4 * g) = v;
+            }
+        }
+    }
+}
+
+template <int MTO>
+void* couple_bwd_ptr_m(int ht) {
+    switch (ht) {
+        case 1: return reinterpret_cast<void*>(&couple_bwd_kernel<1, MTO>);
+        case 2: return reinterpret_cast<void*>(&couple_bwd_kernel<2, MTO>);
+        case 4: return reinterpret_cast<void*>(&couple_bwd_kernel<4, MTO>);
+        case 8: return reinterpret_cast<void*>(&couple_bwd_kernel<8, MTO>);
+        case 16: return reinterpret_cast<void*>(&couple_bwd_kernel<16, MTO>);
+        default: return nullptr;
+    }
+}
+
+void* couple_bwd_ptr(int ht, int mto) { return mto == 2 ? couple_bwd_ptr_m<2>(ht) : couple_bwd_ptr_m<1>(ht); }
 
 // dW = δ · inᵀ and db = Σ δ over this workgroup's contiguous sample range.
 // Both operands are staged sample-major in LDS (row stride ≡ 4 mod 8 floats:
@@ -324,6 +492,7 @@ void* ldense_ptr_mt(int in_kind, int epi) {
         case LEPI_ACT: return reinterpret_cast<void*>(&ldense_kernel<MT, LIN_BUF, LEPI_ACT>);
         case LEPI_COUPLE: return reinterpret_cast<void*>(&ldense_kernel<MT, LIN_BUF, LEPI_COUPLE>);
         case LEPI_DACT: return reinterpret_cast<void*>(&ldense_kernel<MT, LIN_BUF, LEPI_DACT>);
+        case LEPI_DACT_XBAR: return reinterpret_cast<void*>(&ldense_kernel<MT, LIN_BUF, LEPI_DACT_XBAR>);
         default: return reinterpret_cast<void*>(&ldense_kernel<MT, LIN_BUF, LEPI_XBAR>);
     }
 }
@@ -357,7 +526,7 @@ hipError_t ldense_occupancy(int mt, int in_kind, int epi, size_t lds, int* block
 
 hipError_t set_ldense_lds_limit(size_t lds) {
     for (int mt : {1, 2, 4, 8, 16}) {
-        for (int epi = 0; epi < 4; ++epi) {
+        for (int epi = 0; epi < 5; ++epi) {
             hipError_t e = hipFuncSetAttribute(ldense_ptr(mt, LIN_BUF, epi),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
@@ -368,6 +537,23 @@ hipError_t set_ldense_lds_limit(size_t lds) {
     }
     return hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)ldw_lds_bytes());
+}
+
+hipError_t launch_couple_bwd(int ht, int mto, const LDenseArgs& a, unsigned grid, size_t lds, hipStream_t st) {
+    void* k = couple_bwd_ptr(ht, mto);
+    if (!k) return hipErrorInvalidValue;
+    void* args[] = {const_cast<LDenseArgs*>(&a)};
+    return hipLaunchKernel(k, dim3(grid), dim3(kBlockThreads), args, lds, st);
+}
+
+hipError_t set_couple_bwd_lds_limit(size_t lds) {
+    for (int ht : {1, 2, 4, 8, 16})
+        for (int mto : {1, 2}) {
+            hipError_t e = hipFuncSetAttribute(couple_bwd_ptr(ht, mto), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)lds);
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
 }
 
 hipError_t launch_gather_features(const LDenseArgs& a, int rows, hipStream_t st) {

@@ -436,8 +436,11 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         auto H = [&](int k) -> float* {
             return t->hsave_on ? t->d_hsave + ((int64_t)net_slot * t->lmax_h + k) * batch * W : t->d_lh[k];
         };
+        // fused backward front (needs the kept activations, <= 32 outputs, hidden <= 256)
+        const bool fused = t->hsave_on && N.dn[nd - 1].fwd.mt <= 2 && N.dn[0].bwd.mt <= 4 &&
+                           !(std::getenv("DF_TRAIN_NOFUSE") && std::getenv("DF_TRAIN_NOFUSE")[0] == '1');
         // forward (recompute): H_k = σ(W_k · in + b_k), then the output Dense + coupling pullback → ȳ
-        for (int k = 0; k < nd; ++k) {
+        for (int k = 0; k < nd - (fused ? 1 : 0); ++k) {
             LDenseArgs a = b;
             a.act = N.dn[k].act;
             if (k + 1 < nd && t->hsave_on) {
@@ -462,7 +465,54 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         }
         // backward: δ_{k-1} = (W_kᵀ δ_k) ⊙ σ'(H_{k-1}); x̄ = W0ᵀ δ_0 → z̄ (identity dims)
         const float* gcur = t->d_ly;
-        for (int k = nd - 1; k >= 1; --k) {
+        const LDense& DO = N.dn[nd - 1];
+        if (fused) {
+            // output Dense + pullback + (W_outᵀ ȳ) ⊙ σ'(H) in one pass; the last W_kᵀ
+            // product carries x̄ = W0ᵀ δ0 in its epilogue
+            LDenseArgs a = b;
+            a.act = DO.act;
+            a.in = H(nd - 2);
+            a.wfrag = lb + DO.fwd.frag;
+            a.bias = DO.fwd.bias >= 0 ? lbf + DO.fwd.bias : nullptr;
+            a.nkq = DO.fwd.nkq;
+            a.w2frag = lb + DO.bwd.frag;
+            a.nkq2 = DO.bwd.nkq;
+            a.out = t->d_ly;
+            a.out2 = t->d_ld[nd - 2];
+            a.dact = N.dn[nd - 2].act;
+            const size_t lds = (size_t)2 * DO.bwd.mt * DO.fwd.mt * 1024;
+            if (e == hipSuccess) e = launch_couple_bwd(DO.bwd.mt, DO.fwd.mt, a, dgrid, lds, st);
+            gcur = t->d_ld[nd - 2];
+            for (int k = nd - 2; k >= 1; --k) {
+                LDenseArgs c2 = b;
+                c2.in = gcur;
+                c2.hprev = H(k - 1);
+                c2.dact = N.dn[k - 1].act;
+                c2.out = t->d_ld[k - 1];
+                if (k == 1) {
+                    c2.w0t = lb + N.dn[0].bwd.frag;
+                    c2.w0t_mt = N.dn[0].bwd.mt;
+                    c2.w0t_nkq = N.dn[0].bwd.nkq;
+                    const LOp& op = N.dn[k].bwd;
+                    const int nchunks = (op.nkq + op.chunk_kq - 1) / op.chunk_kq;
+                    const size_t lds2 = (size_t)(nchunks > 1 ? 2 : 1) * std::min(op.nkq, op.chunk_kq) * op.mt * 1024 +
+                                        (size_t)c2.w0t_mt * c2.w0t_nkq * 1024;
+                    c2.wfrag = lb + op.frag;
+                    c2.nkq = op.nkq;
+                    c2.chunk_kq = op.chunk_kq;
+                    if (e == hipSuccess) e = launch_ldense(op.mt, LIN_BUF, LEPI_DACT_XBAR, c2, dgrid, lds2, st);
+                } else {
+                    dense(N.dn[k].bwd, LIN_BUF, LEPI_DACT, c2);
+                }
+                gcur = t->d_ld[k - 1];
+            }
+            if (nd == 2) {
+                LDenseArgs c3 = b;
+                c3.in = gcur;
+                dense(N.dn[0].bwd, LIN_BUF, LEPI_XBAR, c3);
+            }
+        }
+        for (int k = nd - 1; k >= 1 && !fused; --k) {
             LDenseArgs a = b;
             a.in = gcur;
             a.hprev = H(k - 1);
@@ -471,7 +521,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             dense(N.dn[k].bwd, LIN_BUF, LEPI_DACT, a);
             gcur = t->d_ld[k - 1];
         }
-        {
+        if (!fused) {
             LDenseArgs a = b;
             a.in = gcur;
             dense(N.dn[0].bwd, LIN_BUF, LEPI_XBAR, a);
@@ -574,7 +624,8 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
     }
     t->grid = std::max(1, c->n_cu * occ);
     if (t->layerwise) {
-        e = set_ldense_lds_limit((size_t)2 * kLChunkBytes);
+        e = set_ldense_lds_limit((size_t)2 * kLChunkBytes + 64 * 1024);
+        if (e == hipSuccess) e = set_couple_bwd_lds_limit(64 * 1024);
         if (e != hipSuccess) {
             df_train_destroy(t);
             return hip_err(e, "hipFuncSetAttribute(layer-wise training)");
