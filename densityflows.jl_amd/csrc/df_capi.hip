@@ -89,8 +89,9 @@ int df_chain_destroy(df_chain* c) {
     if (!c) return DF_OK;
     if (c->n_trainers > 0) return set_err(DF_ERR_INVALID, "df_chain_destroy: destroy its df_train handles first");
     DeviceGuard gd(c->device);
-    void* ptrs[] = {c->d_layers, c->d_denses, c->d_chunks, c->d_stages, c->d_blob,
-                    c->d_tables, c->d_params, c->d_bounds, c->d_partial, c->d_sched, c->d_ulayers};
+    void* ptrs[] = {c->d_layers, c->d_denses, c->d_chunks,  c->d_stages,  c->d_blob,  c->d_tables,
+                    c->d_params, c->d_bounds, c->d_partial, c->d_sched,   c->d_ulayers, c->d_wlayers,
+                    c->d_wstages, c->d_wblob, c->d_wbias,  c->d_wsched};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;
@@ -130,6 +131,17 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
         df_chain_destroy(c);
         return set_err(rc, m);
     }
+    if (P.wide) {
+        std::vector<int32_t> wsched(P.wsched_fwd);
+        wsched.insert(wsched.end(), P.wsched_bwd.begin(), P.wsched_bwd.end());
+        if ((rc = upload(P.wlayers, &c->d_wlayers)) != DF_OK || (rc = upload(P.wstages, &c->d_wstages)) != DF_OK ||
+            (rc = upload(P.wblob, &c->d_wblob)) != DF_OK || (rc = upload(P.wbias, &c->d_wbias)) != DF_OK ||
+            (rc = upload(wsched, &c->d_wsched)) != DF_OK) {
+            std::string m = last_error();
+            df_chain_destroy(c);
+            return set_err(rc, m);
+        }
+    }
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->d_bounds), sizeof(float) * (2 * P.n + 4));
     if (e != hipSuccess) {
         df_chain_destroy(c);
@@ -145,6 +157,15 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
     if (c->lds > 160 * 1024) {
         df_chain_destroy(c);
         return set_err(DF_ERR_UNSUPPORTED, "chain needs more than 160 KiB of LDS per workgroup");
+    }
+    if (P.wide) {
+        c->wide_lds = (size_t)2 * df::kWideStageBytes + c->tab_bytes +
+                      (size_t)df::kWideWaves * 16 * df::kWideT * P.stride * 4;
+        e = df::set_wide_lds_limit(c->wide_lds);
+        if (e != hipSuccess) {
+            df_chain_destroy(c);
+            return hip_err(e, "hipFuncSetAttribute(wide)");
+        }
     }
     e = df::set_kernel_lds_limit(P.ht, P.uniform != 0, c->lds);
     if (e != hipSuccess) {
@@ -238,8 +259,9 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
 
     DeviceGuard gd(c->device);
     if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
-    const int tiles = choose_tiles(c, mode, batch);
-    const int64_t S = (int64_t)df::kWavesPerBlock * 16 * tiles;
+    const bool wide = P.wide && !(std::getenv("DF_NO_WIDE") && std::getenv("DF_NO_WIDE")[0] == '1');
+    const int tiles = wide ? df::kWideT : choose_tiles(c, mode, batch);
+    const int64_t S = wide ? (int64_t)df::kWideWaves * 16 * df::kWideT : (int64_t)df::kWavesPerBlock * 16 * tiles;
     const int64_t grid = (batch + S - 1) / S;
     if (grid > 0x7fffffff) return set_err(DF_ERR_UNSUPPORTED, "batch too large for one launch");
     if (sum_out && grid > c->partial_cap) {
@@ -290,8 +312,21 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     a.hsave_h = hsave_h;
 
     hipStream_t st = static_cast<hipStream_t>(stream);
-    hipError_t e = df::launch_chain(P.ht, mode, P.outv != 0, uniform_variant(P), a, (unsigned)grid,
-                                    lds_for_tiles(c, tiles), st);
+    hipError_t e;
+    if (wide) {
+        a.blob = static_cast<const uint8_t*>(c->d_wblob);
+        a.stages = static_cast<const df::DevStage*>(c->d_wstages);
+        a.sched_fwd = static_cast<const int32_t*>(c->d_wsched);
+        a.sched_bwd = a.sched_fwd + P.wsched_fwd.size();
+        a.n_sched_fwd = (int)P.wsched_fwd.size();
+        a.n_sched_bwd = (int)P.wsched_bwd.size();
+        a.wlayers = static_cast<const df::WLayer*>(c->d_wlayers);
+        a.wbias = static_cast<const float*>(c->d_wbias);
+        e = df::launch_wide(mode, a, (unsigned)grid, c->wide_lds, st);
+    } else {
+        e = df::launch_chain(P.ht, mode, P.outv != 0, uniform_variant(P), a, (unsigned)grid, lds_for_tiles(c, tiles),
+                             st);
+    }
     if (e != hipSuccess) return hip_err(e, "chain kernel launch");
     if (sum_out) {
         e = df::launch_reduce_partials(c->d_partial, grid, sum_out, st);

@@ -35,6 +35,13 @@ struct df_chain {
     int tab_bytes = 0;
     size_t lds = 0;
     int n_trainers = 0;         // live df_train handles bound to this chain
+    // wide-net kernel (plan.wide): its own blob, stages, schedules, descriptors
+    void* d_wlayers = nullptr;
+    void* d_wstages = nullptr;
+    void* d_wblob = nullptr;
+    void* d_wbias = nullptr;
+    void* d_wsched = nullptr;
+    size_t wide_lds = 0;
 };
 
 namespace df {

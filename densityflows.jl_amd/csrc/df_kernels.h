@@ -47,6 +47,8 @@ struct ChainArgs {
     float* hsave;        // inverse modes, generic kernel: hidden activations of every net,
                          // [(layer·2 + net)·hsave_h + k][sample][hsave_w] (training, layer-wise path)
     int hsave_w, hsave_h;
+    const WLayer* wlayers;   // wide-net kernel only (stages / blob / schedules then refer to the wide blob)
+    const float* wbias;
 };
 
 // Per-variant entry points (explicitly instantiated in df_kernels_ht*.hip).
@@ -70,5 +72,9 @@ hipError_t launch_chain(int ht, int mode, bool outv, int uniform, const ChainArg
                         size_t lds, hipStream_t st);
 hipError_t kernel_occupancy(int ht, int mode, bool outv, int uniform, size_t lds, int* blocks);
 hipError_t launch_reduce_partials(const double* part, int64_t n, double* out, hipStream_t st);
+
+// Wide-net kernel (df_wide.hip): 4-wave workgroups of kWideWaves*16*kWideT samples.
+hipError_t launch_wide(int mode, const ChainArgs& a, unsigned grid, size_t lds, hipStream_t st);
+hipError_t set_wide_lds_limit(size_t lds);
 
 }  // namespace df

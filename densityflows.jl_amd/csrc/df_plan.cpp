@@ -116,6 +116,148 @@ void check_net(const df_dense_desc* net, int nd, int in_dim, int out_dim, const 
     }
 }
 
+// Wide-net packing (see WNet).  Leaves P.wide = 0 unless every coupling layer's
+// conditioners are Dense(in <= 64, 256) → Dense(256, 256) → Dense(256, out <= 32).
+void build_wide(const df_chain_desc* desc, Plan& P) {
+    if (const char* f = std::getenv("DF_NO_WIDE"))
+        if (f[0] == '1') return;
+    if (P.uniform || P.ht != 16) return;
+    for (int li = 0; li < desc->n_layers; ++li) {
+        const df_layer_desc& L = desc->layers[li];
+        if (L.kind == DF_LAYER_NORM) continue;
+        auto ok = [&](const df_dense_desc* net, int nd) {
+            return nd == 3 && net[0].in_dim <= kMaxState && net[0].out_dim == 256 && net[1].out_dim == 256 &&
+                   net[2].out_dim <= 32 && net[0].act == DF_ACT_RELU && net[1].act == DF_ACT_RELU &&
+                   net[2].act == DF_ACT_IDENTITY;
+        };
+        if (L.kind == DF_LAYER_RNVP && !ok(L.s_net, L.n_dense_s)) return;
+        if (!ok(L.t_net, L.n_dense_t)) return;
+    }
+    int li_dense = 0;  // running index into P.denses (trainables offsets)
+    std::vector<WLayer> wl;
+    for (int li = 0; li < desc->n_layers; ++li) {
+        const df_layer_desc& L = desc->layers[li];
+        const DevLayer& DL = P.layers[li];
+        WLayer W{};
+        W.kind = DL.kind;
+        W.elem_start = DL.elem_start;
+        W.elem_end = DL.elem_end;
+        W.n_af = DL.n_af;
+        W.feat_tab = DL.feat_tab;
+        W.af_tab = DL.af_tab;
+        W.norm_off = DL.norm_off;
+        W.alpha = DL.alpha;
+        W.beta = DL.beta;
+        W.ldj_const = DL.ldj_const;
+        if (L.kind != DF_LAYER_NORM) {
+            auto pack = [&](const df_dense_desc* net, int d0, WNet& N) {
+                const int ks = (net[0].in_dim + 3) / 4;  // state k-steps: feature k = 4s + g
+                const int nkq0 = (ks + 3) / 4;
+                N.stage0 = (int)P.wstages.size();
+                N.nst0 = (nkq0 + 1) / 2;
+                N.ks = ks;
+                N.n_out = net[2].out_dim;
+                N.mto = (N.n_out + 15) / 16;
+                N.act0 = net[0].act;
+                N.act1 = net[1].act;
+                N.act_out = net[2].act;
+                auto new_stage = [&](int bytes) -> float* {
+                    DevStage st{};
+                    st.src_off = (int64_t)P.wblob.size();
+                    st.bytes = bytes;
+                    P.wstages.push_back(st);
+                    P.wblob.resize(P.wblob.size() + bytes, 0);
+                    return reinterpret_cast<float*>(P.wblob.data() + st.src_off);
+                };
+                auto put = [&](float* base, int64_t q, int dense, int row, int k) {
+                    const df_dense_desc& D = net[dense];
+                    if (row >= D.out_dim || k >= D.in_dim) return;
+                    base[q] = D.W[(size_t)row + (size_t)D.out_dim * k];
+                    const int64_t f0 = (reinterpret_cast<uint8_t*>(base) - P.wblob.data()) / 4;
+                    P.wpack_dst.push_back((int32_t)(f0 + q));
+                    P.wpack_src.push_back(P.denses[d0 + dense].w_off + row + D.out_dim * k);
+                };
+                // first Dense: [kk < 2][m < 16][lane][r], k-step s = 4kq + r, feature 4s + g
+                for (int st = 0; st < N.nst0; ++st) {
+                    float* b = new_stage(kWideStageBytes);
+                    for (int kk = 0; kk < 2; ++kk)
+                        for (int m = 0; m < 16; ++m)
+                            for (int lane = 0; lane < 64; ++lane)
+                                for (int r = 0; r < 4; ++r) {
+                                    const int s = 4 * (2 * st + kk) + r;
+                                    if (s >= ks) continue;
+                                    put(b, ((int64_t)(kk * 16 + m) * 64 + lane) * 4 + r, 0, 16 * m + (lane & 15),
+                                        4 * s + (lane >> 4));
+                                }
+                }
+                // hidden Dense: 8 stages of [kk < 2][m < 16], k = 16kq + 4g + r
+                for (int st = 0; st < 8; ++st) {
+                    float* b = new_stage(kWideStageBytes);
+                    for (int kk = 0; kk < 2; ++kk)
+                        for (int m = 0; m < 16; ++m)
+                            for (int lane = 0; lane < 64; ++lane)
+                                for (int r = 0; r < 4; ++r)
+                                    put(b, ((int64_t)(kk * 16 + m) * 64 + lane) * 4 + r, 1, 16 * m + (lane & 15),
+                                        16 * (2 * st + kk) + 4 * (lane >> 4) + r);
+                }
+                // output Dense: [kq < 16][m < mto]
+                {
+                    float* b = new_stage(16 * N.mto * 1024);
+                    for (int kq = 0; kq < 16; ++kq)
+                        for (int m = 0; m < N.mto; ++m)
+                            for (int lane = 0; lane < 64; ++lane)
+                                for (int r = 0; r < 4; ++r)
+                                    put(b, ((int64_t)(kq * N.mto + m) * 64 + lane) * 4 + r, 2, 16 * m + (lane & 15),
+                                        16 * kq + 4 * (lane >> 4) + r);
+                }
+                auto bias = [&](int dense, int rows) -> int32_t {
+                    const df_dense_desc& D = net[dense];
+                    if (!D.b) return -1;
+                    const int32_t off = (int32_t)P.wbias.size();
+                    P.wbias.resize(P.wbias.size() + rows, 0.f);
+                    for (int r = 0; r < D.out_dim; ++r) {
+                        P.wbias[off + r] = D.b[r];
+                        P.wbias_dst.push_back(off + r);
+                        P.wbias_src.push_back(P.denses[d0 + dense].b_off + r);
+                    }
+                    return off;
+                };
+                N.b0 = bias(0, 256);
+                N.b1 = bias(1, 256);
+                N.bo = bias(2, 16 * N.mto);
+            };
+            if (L.kind == DF_LAYER_RNVP) pack(L.s_net, DL.s_dense0, W.s);
+            pack(L.t_net, DL.t_dense0, W.t);
+        }
+        wl.push_back(W);
+    }
+    (void)li_dense;
+    auto sched = [&](bool fwd) {
+        std::vector<int32_t> out;
+        auto net = [&](const WNet& N) {
+            for (int s = 0; s < N.nst0 + 9; ++s) out.push_back(N.stage0 + s);
+        };
+        for (int it = 0; it < P.n_layers; ++it) {
+            const WLayer& L = wl[fwd ? it : P.n_layers - 1 - it];
+            if (L.kind == DF_LAYER_NORM) continue;
+            if (fwd) {
+                if (L.kind == DF_LAYER_RNVP) net(L.s);
+                net(L.t);
+            } else {
+                net(L.t);
+                if (L.kind == DF_LAYER_RNVP) net(L.s);
+            }
+        }
+        return out;
+    };
+    P.wsched_fwd = sched(true);
+    P.wsched_bwd = sched(false);
+    P.wlayers = std::move(wl);
+    P.wblob.resize(P.wblob.size() + 16, 0);
+    P.wbias.resize(P.wbias.size() + 4, 0.f);
+    P.wide = 1;
+}
+
 }  // namespace
 
 size_t plan_lds_bytes(const Plan& p) {
@@ -621,6 +763,7 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
             P.stage_max = 0;
         }
         P.blob.resize(round_up((int)P.blob.size(), 16) + 16, 0);
+        build_wide(desc, P);
         *out = std::move(P);
         return DF_OK;
     } catch (const Fail& f) {

@@ -104,6 +104,30 @@ struct ULayer {
     UNet s, t;
 };
 
+// Wide-net kernel (df_wide_impl.h): every conditioner is Dense(in <= 64, 256) →
+// Dense(256, 256) → Dense(256, out <= 32).  Its weights live in their own blob of
+// fixed 32 KiB stages: first Dense (2 k-quads × 16 m-tiles per stage), 8 stages of
+// the hidden Dense, one stage of the output Dense ([kq < 16][m < mto]).
+constexpr int kWideStageBytes = 32 * 1024;
+constexpr int kWideWaves = 4;     // one wave per SIMD (512 registers each)
+constexpr int kWideT = 2;         // 16-sample tiles per wave held in registers (3 spills)
+
+struct WNet {
+    int32_t stage0;   // first stage id (wide blob)
+    int32_t nst0;     // stages of the first Dense (1 or 2)
+    int32_t ks;       // first-Dense k-steps (ceil(in/4))
+    int32_t n_out, mto;
+    int32_t act0, act1, act_out;
+    int32_t b0, b1, bo;  // float offsets of the (padded) biases in wbias, -1: none
+};
+
+struct WLayer {
+    int32_t kind, elem_start, elem_end, n_af;
+    int32_t feat_tab, af_tab, norm_off, pad0;
+    float alpha, beta, ldj_const, pad1;
+    WNet s, t;
+};
+
 struct DevStage {
     int64_t src_off;     // byte offset in the blob
     int32_t bytes;       // multiple of 16
@@ -136,6 +160,15 @@ struct Plan {
     std::vector<float> trainables;
     // blob float index ← trainables index, for every blob float that holds a parameter
     std::vector<int32_t> pack_dst, pack_src;
+    // wide-net kernel (empty unless every conditioner has the wide default shape)
+    int wide = 0;
+    std::vector<WLayer> wlayers;
+    std::vector<DevStage> wstages;
+    std::vector<uint8_t> wblob;
+    std::vector<float> wbias;
+    std::vector<int32_t> wsched_fwd, wsched_bwd;
+    std::vector<int32_t> wpack_dst, wpack_src;   // wblob float index ← trainables index
+    std::vector<int32_t> wbias_dst, wbias_src;   // wbias index ← trainables index
     double flops_per_sample = 0.0;
 };
 

@@ -104,6 +104,11 @@ struct df_train {
     // skips the forward recompute.  [(layer·2 + net)·lmax_h + k][B][lwidth]
     float* d_hsave = nullptr;
     bool hsave_on = false;
+    // repack maps of the chain's wide-kernel blob and biases (plan.wide)
+    void* d_wdst = nullptr;
+    void* d_wsrc = nullptr;
+    void* d_wbdst = nullptr;
+    void* d_wbsrc = nullptr;
 };
 
 namespace {
@@ -111,7 +116,8 @@ namespace {
 void free_all(df_train* t) {
     void* ptrs[] = {t->d_params, t->d_m,    t->d_v,    t->d_grad, t->d_partial, t->d_tblob, t->d_pdst,
                     t->d_psrc,   t->d_tdst, t->d_tsrc, t->d_snap, t->d_zbar,    t->d_ebuf,  t->d_lpsum,
-                    t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_ly,   t->d_lx,      t->d_hsave};
+                    t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_ly,   t->d_lx,      t->d_hsave,
+                    t->d_wdst,   t->d_wsrc, t->d_wbdst, t->d_wbsrc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (float* p : t->d_lh)
@@ -374,6 +380,13 @@ int repack(df_train* t, hipStream_t st) {
     if (e == hipSuccess && !t->tdst.empty())
         e = launch_repack(static_cast<float*>(t->d_tblob), static_cast<const int32_t*>(t->d_tdst),
                           static_cast<const int32_t*>(t->d_tsrc), (int64_t)t->tdst.size(), t->d_params, st);
+    if (e == hipSuccess && P.wide) {
+        e = launch_repack(static_cast<float*>(c->d_wblob), static_cast<const int32_t*>(t->d_wdst),
+                          static_cast<const int32_t*>(t->d_wsrc), (int64_t)P.wpack_dst.size(), t->d_params, st);
+        if (e == hipSuccess)
+            e = launch_repack(static_cast<float*>(c->d_wbias), static_cast<const int32_t*>(t->d_wbdst),
+                              static_cast<const int32_t*>(t->d_wbsrc), (int64_t)P.wbias_dst.size(), t->d_params, st);
+    }
     if (e == hipSuccess && !t->ldst.empty())
         e = launch_repack(static_cast<float*>(t->d_lblob), static_cast<const int32_t*>(t->d_ldst),
                           static_cast<const int32_t*>(t->d_lsrc), (int64_t)t->ldst.size(), t->d_params, st);
@@ -645,7 +658,9 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
     }
     if ((rc = upload(t->tblob, &t->d_tblob)) != DF_OK || (rc = upload(t->lblob, &t->d_lblob)) != DF_OK ||
         (rc = upload(t->ldst, &t->d_ldst)) != DF_OK || (rc = upload(t->lsrc, &t->d_lsrc)) != DF_OK ||
-        (rc = upload(P.pack_dst, &t->d_pdst)) != DF_OK ||
+        (rc = upload(P.pack_dst, &t->d_pdst)) != DF_OK || (rc = upload(P.wpack_dst, &t->d_wdst)) != DF_OK ||
+        (rc = upload(P.wpack_src, &t->d_wsrc)) != DF_OK || (rc = upload(P.wbias_dst, &t->d_wbdst)) != DF_OK ||
+        (rc = upload(P.wbias_src, &t->d_wbsrc)) != DF_OK ||
         (rc = upload(P.pack_src, &t->d_psrc)) != DF_OK || (rc = upload(t->tdst, &t->d_tdst)) != DF_OK ||
         (rc = upload(t->tsrc, &t->d_tsrc)) != DF_OK) {
         std::string m = last_error();

@@ -1,0 +1,427 @@
+// df_wide_impl.h — the wide-net chain kernel: every conditioner is the default
+// _dflt_net shape at hidden width 256 (src/Layers.jl:33-50):
+//   Dense(in <= 64, 256, relu) → Dense(256, 256, relu) → Dense(256, out <= 32)
+// (the default σ; other activations run on the generic kernel).
+// BASELINE configs 4/5 (d = 32, n = 8, hidden 256).
+//
+// Why a separate kernel: at hidden 256 one 16-sample tile needs 64 registers of
+// activations plus 64 of accumulators, so the generic kernel (8 waves, 2 per SIMD,
+// 256 registers each) holds ONE tile per wave and every 64 KiB weight stage feeds
+// 128 samples per CU.  Here a workgroup is 4 waves — one per SIMD, 512 registers
+// each (accumulators in AGPRs) — and each wave keeps 3 tiles resident, so a stage
+// feeds 192 samples and every A-fragment read feeds 12 MFMAs instead of 4.  The
+// weights live in their own blob of fixed 32 KiB stages (first Dense, 8 hidden
+// stages, output Dense), double-buffered in LDS by global→LDS DMA in a fixed
+// order, so every k-quad index is a compile-time constant (no guards, no
+// dynamic register indexing).  Numerics as the other kernels: -ffp-contract=off,
+// bias after the product, exact MFMA fma chains, same relu/exp.
+#pragma once
+
+#include "df_chain_impl.h"
+#include "df_uniform_impl.h"
+
+namespace df {
+namespace wide {
+
+using impl::lds4;
+using impl::mfma4;
+
+constexpr int kThreads = kWideWaves * 64;
+constexpr int T = kWideT;
+
+struct WStager {
+    uint8_t* base;
+    const int32_t* sched;
+    int n;
+    int idx;
+    int cur;
+    __device__ __forceinline__ uint8_t* buf() const { return base + ((idx & 1) ? kWideStageBytes : 0); }
+};
+
+__device__ __forceinline__ void dma(const ChainArgs& a, int s, uint8_t* dst) {
+    const DevStage st = a.stages[s];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint8_t* src = a.blob + st.src_off;
+    const int nchunk = st.bytes >> 10;
+    for (int c = wave; c < nchunk; c += kWideWaves)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (c << 10) + lane * 16),
+                                         (__attribute__((address_space(3))) void*)(dst + (c << 10)), 16, 0, 0);
+}
+
+// Stage s, which is the next one of the fixed schedule, becomes resident; the one
+// after it is put in flight into the other buffer.
+__device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
+    if (s == sg.cur) return;
+    const int nidx = sg.idx + 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    sg.idx = nidx;
+    sg.cur = s;
+    if (nidx >= sg.n || sg.sched[nidx] != s) {  // off schedule (never produced by the planner)
+        const DevStage st = a.stages[s];
+        const f32x4* src = reinterpret_cast<const f32x4*>(a.blob + st.src_off);
+        f32x4* dst = reinterpret_cast<f32x4*>(sg.buf());
+        for (int i = threadIdx.x; i < (st.bytes >> 4); i += kThreads) dst[i] = src[i];
+        __syncthreads();
+        sg.n = 0;
+        return;
+    }
+    if (nidx + 1 < sg.n) dma(a, sg.sched[nidx + 1], sg.base + (((nidx + 1) & 1) ? kWideStageBytes : 0));
+}
+
+// h = σ.(acc .+ b)  (b: 256 floats in global memory, L2-resident)
+__device__ __forceinline__ void bias_act(const float* b, int act, const f32x4 (&acc)[T][16], f32x4 (&h)[T][16]) {
+    const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const f32x4 bb = b ? *reinterpret_cast<const f32x4*>(b + 16 * m + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            f32x4 v = acc[t][m];
+            if (b) v = v + bb;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = uni::relu_fast(v[r]);  // planner: σ0 = σ1 = relu
+            h[t][m] = v;
+        }
+    }
+}
+
+// Evaluate net N for this wave's T tiles (state rows ro[t]) into out[t][0..1]
+// (rows 16m + 4g + r).  hs: training, keep H0 / H1 (sample-major, width hsave_w).
+__device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, const int32_t* feat,
+                                         const float* state, const int (&ro)[T], WStager& sg, f32x4 (&out)[T][2],
+                                         float* hs, const int64_t (&gs)[T]) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    f32x4 h[T][16], acc[T][16];
+
+    // ---- first Dense: features vcat(θ, z)[axis_nn] from the LDS state, k = 4s + g ----
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+        if (st < N.nst0) {
+            ensure(N.stage0 + st, sg, a);
+            const uint8_t* buf = sg.buf() + lane * 16;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const int kq = 2 * st + kk;
+                const int rmax = N.ks - 4 * kq;  // k-steps of this k-quad carrying features
+                if (rmax > 0) {
+                    float xin[T][4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int slot = (r < rmax) ? feat[4 * (4 * kq + r) + g] : 0;
+#pragma unroll
+                        for (int t = 0; t < T; ++t) xin[t][r] = (r < rmax) ? state[ro[t] + slot] : 0.f;
+                    }
+#pragma unroll
+                    for (int m0 = 0; m0 < 16; m0 += 4) {
+                        f32x4 w[4];
+#pragma unroll
+                        for (int mm = 0; mm < 4; ++mm) w[mm] = lds4(buf + (kk * 16 + m0 + mm) * 1024);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (r < rmax)
+#pragma unroll
+                                for (int mm = 0; mm < 4; ++mm)
+#pragma unroll
+                                    for (int t = 0; t < T; ++t)
+                                        acc[t][m0 + mm] = mfma4(w[mm][r], xin[t][r], acc[t][m0 + mm]);
+                    }
+                }
+            }
+        }
+    }
+    bias_act(N.b0 >= 0 ? a.wbias + N.b0 : nullptr, N.act0, acc, h);
+    if (hs) {
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+            if (gs[t] >= 0)
+#pragma unroll
+                for (int m = 0; m < 16; ++m)
+                    *reinterpret_cast<f32x4*>(hs + gs[t] * a.hsave_w + 16 * m + 4 * g) = h[t][m];
+    }
+
+    // ---- hidden Dense 256×256: 8 stages of 2 k-quads ----
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+        ensure(N.stage0 + N.nst0 + st, sg, a);
+        const uint8_t* buf = sg.buf() + lane * 16;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int kq = 2 * st + kk;
+#pragma unroll
+            for (int m0 = 0; m0 < 16; m0 += 4) {
+                f32x4 w[4];
+#pragma unroll
+                for (int mm = 0; mm < 4; ++mm) w[mm] = lds4(buf + (kk * 16 + m0 + mm) * 1024);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int mm = 0; mm < 4; ++mm)
+#pragma unroll
+                        for (int t = 0; t < T; ++t) acc[t][m0 + mm] = mfma4(w[mm][r], h[t][kq][r], acc[t][m0 + mm]);
+            }
+        }
+    }
+    bias_act(N.b1 >= 0 ? a.wbias + N.b1 : nullptr, N.act1, acc, h);
+    if (hs) {
+        float* hs1 = hs + a.batch * a.hsave_w;
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+            if (gs[t] >= 0)
+#pragma unroll
+                for (int m = 0; m < 16; ++m)
+                    *reinterpret_cast<f32x4*>(hs1 + gs[t] * a.hsave_w + 16 * m + 4 * g) = h[t][m];
+    }
+
+    // ---- output Dense (<= 32 outputs): [kq < 16][m < mto] ----
+    ensure(N.stage0 + N.nst0 + 8, sg, a);
+    const uint8_t* buf = sg.buf() + lane * 16;
+#pragma unroll
+    for (int t = 0; t < T; ++t) out[t][0] = out[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (N.mto == 2) {
+#pragma unroll
+        for (int kq = 0; kq < 16; ++kq) {
+            const f32x4 w0 = lds4(buf + (kq * 2) * 1024), w1 = lds4(buf + (kq * 2 + 1) * 1024);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    out[t][0] = mfma4(w0[r], h[t][kq][r], out[t][0]);
+                    out[t][1] = mfma4(w1[r], h[t][kq][r], out[t][1]);
+                }
+        }
+    } else {
+#pragma unroll
+        for (int kq = 0; kq < 16; ++kq) {
+            const f32x4 w0 = lds4(buf + kq * 1024);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int t = 0; t < T; ++t) out[t][0] = mfma4(w0[r], h[t][kq][r], out[t][0]);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        if (m < N.mto) {
+            const f32x4 bb = (N.bo >= 0) ? *reinterpret_cast<const f32x4*>(a.wbias + N.bo + 16 * m + 4 * g)
+                                         : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                f32x4 v = out[t][m];
+                if (N.bo >= 0) v = v + bb;  // planner: σo = identity
+                out[t][m] = v;
+            }
+        }
+    }
+}
+
+// Coupling phase on the transformed dims (row o = 16m + 4g + r of out ↔ axis_af[o]);
+// sum[t] = Σ_o s_o for the s phases.
+template <int PH>
+__device__ __forceinline__ void couple(const f32x4 (&out)[T][2], const WLayer& L, const int32_t* tab, float* state,
+                                       const int (&ro)[T], float (&sum)[T]) {
+    const int g = (threadIdx.x & 63) >> 4;
+    constexpr bool SPH = (PH == impl::PH_S_FWD || PH == impl::PH_S_BWD);
+    const int32_t* af = tab + L.af_tab;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        float p = 0.f;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int o = 16 * m + 4 * g + r;
+                if (o < L.n_af) {
+                    const int slot = af[o];
+                    const float y = out[t][m][r];
+                    state[ro[t] + slot] = uni::couple1<PH>(state[ro[t] + slot], y);
+                    if (SPH) p = p + y;
+                }
+            }
+        sum[t] = SPH ? uni::xgroup_sum(p) : 0.f;
+    }
+}
+
+}  // namespace wide
+
+template <int MODE>
+__global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
+    using namespace wide;
+    constexpr bool FWD = (MODE == MODE_FWD || MODE == MODE_FWD_INPLACE);
+    constexpr bool WANT_LDJ = (MODE != MODE_FWD_INPLACE);
+
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int stage_area = 2 * kWideStageBytes;
+    int32_t* tab = reinterpret_cast<int32_t*>(smem + stage_area);
+    float* state = reinterpret_cast<float*>(smem + stage_area + a.tab_bytes);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, j = lane & 15;
+    const int d = a.d, n = a.n, stride = a.stride, nd = n + d;
+    constexpr int S = kWideWaves * 16 * T;
+    const int cA = nd + 1, cE = nd + 2;
+    const int64_t s0 = (int64_t)blockIdx.x * S;
+    const int nvalid = (int)((a.batch - s0) < S ? (a.batch - s0) : S);
+
+    WStager sg;
+    sg.base = smem;
+    sg.sched = FWD ? a.sched_fwd : a.sched_bwd;
+    sg.n = FWD ? a.n_sched_fwd : a.n_sched_bwd;
+    sg.idx = -1;
+    sg.cur = -1;
+    if (sg.n > 0) dma(a, sg.sched[0], sg.base);
+
+    for (int i = tid; i < a.tab_ints; i += kThreads) tab[i] = a.tables[i];
+    for (int i = tid; i < S * d; i += kThreads) {
+        const int smp = i / d, c = i - smp * d;
+        state[smp * stride + n + c] = (smp < nvalid) ? a.zin[(s0 + smp) * d + c] : 0.f;
+    }
+    for (int i = tid; i < S * n; i += kThreads) {
+        const int smp = i / n, c = i - smp * n;
+        float v = 0.f;
+        if (smp < nvalid) {
+            v = a.theta[(s0 + smp) * n + c];
+            if (a.tmin) {  // normalize_input (Data.jl:213-218)
+                const float lo = a.tmin[c], diff = a.tmax[c] - lo;
+                v = (diff == 0.f) ? 0.f : (v - lo) / diff;
+            }
+        }
+        state[smp * stride + c] = v;
+    }
+    for (int i = tid; i < S; i += kThreads)
+        for (int c = nd; c < stride; ++c) state[i * stride + c] = 0.f;
+    __syncthreads();
+
+    int ro[T];
+    int64_t gs[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int smp = (wave * T + t) * 16 + j;
+        ro[t] = smp * stride;
+        gs[t] = smp < nvalid ? s0 + smp : -1;
+    }
+    bool have_acc = false;
+    auto ldj_update = [&](int r, float l, bool first_in_elem, bool last_in_elem) {
+        if (!WANT_LDJ || g != 0) return;
+        const float e = first_in_elem ? l : state[r + cE] + l;
+        state[r + cE] = e;
+        if (last_in_elem) state[r + cA] = have_acc ? state[r + cA] + e : e;
+    };
+
+    for (int it = 0; it < a.n_layers; ++it) {
+        const int li = FWD ? it : a.n_layers - 1 - it;
+        const WLayer& L = a.wlayers[li];
+        const bool first_in_elem = FWD ? L.elem_start : L.elem_end;
+        const bool last_in_elem = FWD ? L.elem_end : L.elem_start;
+        if (L.kind == DF_LAYER_NORM) {
+            // NormalizationLayer, src/norm/Normalization.jl:64-103
+            const float al = L.alpha, be = L.beta, delta = be - al;
+            const float* xmn = a.params + L.norm_off;
+            const float* xmx = xmn + d;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                for (int i = g; i < d; i += 4) {
+                    const float lo = xmn[i], hi = xmx[i], xd = hi - lo;
+                    float v = state[ro[t] + n + i];
+                    if (FWD) v = ((xd * v - al * hi) + be * lo) / delta;
+                    else v = (be * (v - lo) + al * (hi - v)) / xd;
+                    state[ro[t] + n + i] = v;
+                }
+                ldj_update(ro[t], FWD ? L.ldj_const : -L.ldj_const, first_in_elem, last_in_elem);
+            }
+        } else {
+            const bool rnvp = (L.kind == DF_LAYER_RNVP);
+            const int32_t* feat = tab + L.feat_tab;
+            float* hs_s = nullptr;
+            float* hs_t = nullptr;
+            if (!FWD && a.hsave) {
+                hs_s = a.hsave + (int64_t)(2 * li) * a.hsave_h * a.batch * a.hsave_w;
+                hs_t = hs_s + (int64_t)a.hsave_h * a.batch * a.hsave_w;
+            }
+            auto run = [&](const WNet& N, auto ph_tag, float* hs, bool sphase, float sign) {
+                constexpr int PH = decltype(ph_tag)::value;
+                f32x4 out[T][2];
+                float sum[T];
+                eval_net(a, N, feat, state, ro, sg, out, hs, gs);
+                couple<PH>(out, L, tab, state, ro, sum);
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    if (sphase) ldj_update(ro[t], sign * sum[t], first_in_elem, last_in_elem);
+                    else if (!rnvp) ldj_update(ro[t], 0.f, first_in_elem, last_in_elem);
+                }
+            };
+            using PSF = std::integral_constant<int, impl::PH_S_FWD>;
+            using PTF = std::integral_constant<int, impl::PH_T_FWD>;
+            using PTB = std::integral_constant<int, impl::PH_T_BWD>;
+            using PSB = std::integral_constant<int, impl::PH_S_BWD>;
+            if (FWD) {
+                if (rnvp) run(L.s, PSF{}, nullptr, true, 1.f);
+                run(L.t, PTF{}, nullptr, false, 1.f);
+            } else {
+                run(L.t, PTB{}, hs_t, false, 1.f);
+                if (rnvp) run(L.s, PSB{}, hs_s, true, -1.f);  // ln_det_jac = -Σ s
+            }
+        }
+        have_acc = have_acc || last_in_elem;
+        if (!FWD && a.snap) {  // training: keep every layer's output for the reverse sweep
+            float* dst = a.snap + (int64_t)li * a.batch * d;
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+                if (gs[t] >= 0)
+                    for (int i = g; i < d; i += 4) dst[gs[t] * d + i] = state[ro[t] + n + i];
+        }
+    }
+
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (MODE == MODE_LOGPDF) {
+        double part = 0.0;
+        if (g == 0) {
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                float q = 0.f;
+                for (int i = 0; i < d; ++i) {
+                    const float zz = state[ro[t] + n + i];
+                    q = q + zz * zz;
+                }
+                const float lp = (a.c0 - q / 2.f) + state[ro[t] + cA];
+                if (gs[t] >= 0) {
+                    if (a.lp_out) a.lp_out[gs[t]] = lp;
+                    part += (double)lp;
+                }
+            }
+        }
+        if (a.partial) {
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off);
+            __syncthreads();
+            double* red = reinterpret_cast<double*>(smem);
+            if (lane == 0) red[wave] = part;
+            __syncthreads();
+            if (tid == 0) {
+                double s = 0.0;
+                for (int w = 0; w < kWideWaves; ++w) s += red[w];
+                a.partial[blockIdx.x] = s;
+            }
+        }
+        if (!a.xout) return;
+    }
+    __syncthreads();
+    for (int i = tid; i < S * d; i += kThreads) {
+        const int smp = i / d, c = i - smp * d;
+        if (smp < nvalid) a.xout[(s0 + smp) * d + c] = state[smp * stride + n + c];
+    }
+    if (WANT_LDJ && MODE != MODE_LOGPDF && a.ldj_out) {
+        for (int i = tid; i < nvalid; i += kThreads) a.ldj_out[s0 + i] = state[i * stride + cA];
+    }
+}
+
+}  // namespace df
