@@ -133,8 +133,8 @@ def cpu_baseline(chain, d, n, seconds=12.0, sample=65536):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--batch", type=int, default=None,
                     help="samples per GPU (default: the config's: 2^20 for cfg1/cfg2, 2^18 for cfg4 = configs[3] "
                          "and the per-GPU share of configs[4])")
