@@ -41,7 +41,7 @@ using namespace df::api;
 
 static size_t lds_for_tiles(const df_chain* c, int t);
 
-static int uniform_variant(const df::Plan& P) { return P.uniform ? (P.relu_only ? 2 : 1) : 0; }
+static int uniform_variant(const df::Plan& P) { return P.uniform ? (P.fast ? 3 : P.relu_only ? 2 : 1) : 0; }
 
 static size_t lds_for_tiles(const df_chain* c, int t) {
     const df::Plan& P = c->plan;

@@ -369,6 +369,33 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
             uniform_shape = uniform_shape && ok_net(L.t_net, L.n_dense_t);
         }
 
+        // ---------- pass 1c: first-Dense bias folding (specialised kernel) ----------
+        // With in < 4·ks the compact first Dense has a free k-slot; the LAST one
+        // (k = 4·ks − 1) carries the bias against a state column that holds 1, so the
+        // MFMA chain ends with fma(b, 1, Σ_k W x) = round(W*x + b): bit-identical to
+        // the separate `W*x .+ b` (Flux) add it replaces.  Both nets of a layer share
+        // the feature table, so a layer folds only when all of its nets have a bias.
+        std::vector<char> fold(desc->n_layers, 0);
+        bool allow_fold = uniform_shape, fold_all = true, any_fold = false, ks1_all = true;
+        if (const char* e = std::getenv("DF_NO_FOLD"))
+            if (e[0] == '1') allow_fold = false;
+        for (int li = 0; li < desc->n_layers; ++li) {
+            const df_layer_desc& L = desc->layers[li];
+            if (L.kind == DF_LAYER_NORM) continue;
+            const int ks = (L.n_nn + 3) / 4;
+            const bool f = allow_fold && L.n_nn < 4 * ks && L.t_net[0].b != nullptr &&
+                           (L.kind != DF_LAYER_RNVP || L.s_net[0].b != nullptr);
+            fold[li] = f ? 1 : 0;
+            any_fold = any_fold || f;
+            fold_all = fold_all && f;
+            ks1_all = ks1_all && ks == 1;
+        }
+        const int one_slot = n + d + 3;
+        if (any_fold) {  // [θ | z | 0 | ldj_chain | ldj_elem | 1]
+            P.stride = n + d + 4;
+            if (P.stride % 2 == 0) P.stride += 1;
+        }
+
         // ---------- pass 2: packing ----------
         // Whole chain in one stage when it is small (loaded once per workgroup);
         // otherwise 24 KiB stages, double-buffered in LDS, one net per stage
@@ -445,7 +472,8 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
             // feature table [ks*4]: k = 4s + g → state slot of vcat(θ,z)[axis_nn[k]]
             DL.feat_tab = (int)P.tables.size();
             for (int k = 0; k < ks_state * 4; ++k)
-                P.tables.push_back(k < L.n_nn ? L.axis_nn[k] - 1 : zero_slot);
+                P.tables.push_back(k < L.n_nn ? L.axis_nn[k] - 1
+                                              : (fold[li] && k == 4 * ks_state - 1) ? one_slot : zero_slot);
             DL.af_tab = (int)P.tables.size();
             for (int k = 0; k < L.n_af; ++k) P.tables.push_back(n + L.axis_af[k] - 1);
 
@@ -574,8 +602,12 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                     if (DD.compact) {  // [m][r < ks][lane]: k = 4r + g
                         for (int m = 0; m < DD.mt; ++m)
                             for (int r = 0; r < DD.ks; ++r)
-                                for (int lane = 0; lane < 64; ++lane)
-                                    Wp(&dst[(m * DD.ks + r) * 64 + lane], 16 * m + (lane & 15), 4 * r + (lane >> 4));
+                                for (int lane = 0; lane < 64; ++lane) {
+                                    const int k = 4 * r + (lane >> 4), row = 16 * m + (lane & 15);
+                                    float* at = &dst[(m * DD.ks + r) * 64 + lane];
+                                    if (fold[li] && k == 4 * DD.ks - 1) Bp(at, row);  // bias · state[one_slot]
+                                    else Wp(at, row, k);
+                                }
                         continue;
                     }
                     // fragment [m][lane][r] for k-quad kq
@@ -681,6 +713,9 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
         // Specialised-kernel descriptors when every net has the default shape.
         P.uniform = (uniform_shape && resident) ? 1 : 0;
         P.relu_only = (P.uniform && relu_only) ? 1 : 0;
+        P.fast = (P.relu_only && allow_fold && fold_all && ks1_all) ? 1 : 0;
+        if (const char* f = std::getenv("DF_NO_FAST"))
+            if (f[0] == '1') P.fast = 0;
         if (uniform_shape && !resident) fail(DF_ERR_UNSUPPORTED, "internal: default-shape net split across stages");
         auto make_unet = [&](int d0, int nd, UNet* u) -> bool {
             if (nd < 2) return false;
@@ -741,6 +776,7 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
                     bool ok = make_unet(L.t_dense0, L.t_ndense, &U.t);
                     if (L.kind == DF_LAYER_RNVP) ok = ok && make_unet(L.s_dense0, L.s_ndense, &U.s);
                     if (!ok) fail(DF_ERR_UNSUPPORTED, "internal: default-shape net with an irregular layout");
+                    U.s.fold0 = U.t.fold0 = fold[P.ulayers.size()];
                 }
                 P.ulayers.push_back(U);
             }

@@ -95,6 +95,7 @@ struct UNet {
     int32_t off_h, hstride;   // hidden k: W at off_h + k*hstride, bias right after W
     int32_t off_out;          // VALU: W[n_out][H] then b[4]; MFMA: frags then bias
     int32_t act0, acth, act_out;
+    int32_t fold0;            // first-Dense bias folded into k-slot 4·ks−1 (state column n+d+3 holds 1)
 };
 
 struct ULayer {
@@ -142,6 +143,7 @@ struct Plan {
     int outv = 0;            // kernel variant: final Dense as VALU GEMV (<= 4 outputs)
     int uniform = 0;         // every layer fits the specialised kernel (ulayers valid)
     int relu_only = 0;       // specialised kernel variant: hidden σ = relu, output σ = identity
+    int fast = 0;            // specialised kernel variant: relu_only, every first Dense one k-step with its bias folded
     std::vector<ULayer> ulayers;
     int samples_per_block = 0;
     int stage_max = 0;       // largest stage (bytes, multiple of kStageAlign)

@@ -137,6 +137,8 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
                     }
                 } else if (slot < n + d) {
                     v = a.u_in[s * d + (slot - n)];
+                } else if (slot == n + d + 3) {
+                    v = 1.f;  // folded first-Dense bias (df_plan.cpp pass 1c)
                 }
             }
             xin[0][r] = v;
@@ -145,7 +147,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
         // ---- forward recompute ----
         f32x4 A0[1][HT], A1[1][HT];
         uni::dense_first<HT, 1>(fw, N, xin, A0);
-        uni::bias_act<HT, 1, RELU>(fw + N.off_b0, N.act0, A0);
+        uni::bias_act<HT, 1, RELU>(fw + N.off_b0, N.act0, A0, !N.fold0);
         if constexpr (NH == 1) {
             uni::dense_hidden<HT, 1>(fw + N.off_h, A0, A1);
             uni::bias_act<HT, 1, RELU>(fw + N.off_h + HT * HT * 1024, N.acth, A1);

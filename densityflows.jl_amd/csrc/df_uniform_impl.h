@@ -40,12 +40,30 @@ constexpr int kTT = kUniformTileGroup;  // 16-sample tiles evaluated together in
 
 // acc = W·x, x = the state features vcat(θ,z)[axis_nn] (<= 16 of them).
 // Compact fragments: [m][r < ks][lane] f32, k = 4r + lane_group.
-template <int HT, int TT>
+// KS > 0: the chain-wide k-step count is a compile-time constant (FAST variant).
+template <int HT, int TT, int KS = 0>
 __device__ __forceinline__ void dense_first(const uint8_t* buf, const UNet& N, const float (&xin)[TT][4],
                                             f32x4 (&acc)[TT][HT]) {
     const int lane = threadIdx.x & 63;
     const float* wb = reinterpret_cast<const float*>(buf + N.off_w0) + lane;
-    const int ks = N.ks;
+    const int ks = KS > 0 ? KS : N.ks;
+    if constexpr (KS > 0) {  // first k-step starts from an inline-zero accumulator
+#pragma unroll
+        for (int m = 0; m < HT; ++m) {
+            const float w = wb[m * KS * 64];
+#pragma unroll
+            for (int t = 0; t < TT; ++t) acc[t][m] = mfma4(w, xin[t][0], f32x4{0.f, 0.f, 0.f, 0.f});
+        }
+#pragma unroll
+        for (int r = 1; r < KS; ++r)
+#pragma unroll
+            for (int m = 0; m < HT; ++m) {
+                const float w = wb[(m * KS + r) * 64];
+#pragma unroll
+                for (int t = 0; t < TT; ++t) acc[t][m] = mfma4(w, xin[t][r], acc[t][m]);
+            }
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < TT; ++t)
 #pragma unroll
@@ -99,15 +117,18 @@ __device__ __forceinline__ void dense_hidden(const uint8_t* wb, const f32x4 (&in
     }
 }
 
-// v = σ.(v .+ b)  — bias after the product (Flux: W*x .+ b)
+// v = σ.(v .+ b)  — bias after the product (Flux: W*x .+ b).  add_bias false:
+// the bias is already the last term of the MFMA chain (folded first Dense).
 template <int HT, int TT, bool RELU>
-__device__ __forceinline__ void bias_act(const uint8_t* bb, int act, f32x4 (&v)[TT][HT]) {
+__device__ __forceinline__ void bias_act(const uint8_t* bb, int act, f32x4 (&v)[TT][HT], bool add_bias = true) {
     const int g = (threadIdx.x & 63) >> 4;
+    if (add_bias) {
 #pragma unroll
-    for (int m = 0; m < HT; ++m) {
-        const f32x4 b = lds4(bb + ((16 * m + 4 * g) << 2));
+        for (int m = 0; m < HT; ++m) {
+            const f32x4 b = lds4(bb + ((16 * m + 4 * g) << 2));
 #pragma unroll
-        for (int t = 0; t < TT; ++t) v[t][m] = v[t][m] + b;
+            for (int t = 0; t < TT; ++t) v[t][m] = v[t][m] + b;
+        }
     }
     if (RELU || act == DF_ACT_RELU) {
 #pragma unroll
@@ -274,7 +295,7 @@ __device__ __forceinline__ void tail(const uint8_t* buf, const UNet& N, const UL
 
 // Evaluate net N for TT 16-sample tiles (state rows ro[t]) and apply its
 // coupling phase; sum[t] = Σ_k s_k for s phases (row order).
-template <int HT, int TT, bool OUTV, bool RELU, int PH>
+template <int HT, int TT, bool OUTV, bool RELU, int PH, bool FAST = false>
 __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, const ULayer& L, const int32_t* tab,
                                           float* state, const int (&ro)[TT], float (&sum)[TT]) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
@@ -282,16 +303,18 @@ __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, con
     // conditioner input: features k = 4r + g of vcat(θ,z)[axis_nn] (zero slot pads)
     float xin[TT][4];
     const int32_t* feat = tab + L.feat_tab;
+    constexpr int KS = FAST ? 1 : 0;
+    const int ks = FAST ? 1 : N.ks;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const int slot = (r < N.ks) ? feat[4 * r + g] : 0;
+        const int slot = (r < ks) ? feat[4 * r + g] : 0;
 #pragma unroll
-        for (int t = 0; t < TT; ++t) xin[t][r] = (r < N.ks) ? state[ro[t] + slot] : 0.f;
+        for (int t = 0; t < TT; ++t) xin[t][r] = (r < ks) ? state[ro[t] + slot] : 0.f;
     }
 
     f32x4 A[TT][HT], B[TT][HT];
-    dense_first<HT, TT>(buf, N, xin, A);
-    bias_act<HT, TT, RELU>(buf + N.off_b0, N.act0, A);
+    dense_first<HT, TT, KS>(buf, N, xin, A);
+    bias_act<HT, TT, RELU>(buf + N.off_b0, N.act0, A, FAST ? false : !N.fold0);
     if (N.nh == 1) {  // the default _dflt_net (n_sublayers = 2): one H×H Dense
         dense_hidden<HT, TT>(buf + N.off_h, A, B);
         bias_act<HT, TT, RELU>(buf + N.off_h + HT * HT * 1024, N.acth, B);
@@ -320,7 +343,7 @@ __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, con
 #define DF_UNI_WAVES 4
 #endif
 
-template <int HT, int MODE, bool OUTV, bool RELU>
+template <int HT, int MODE, bool OUTV, bool RELU, bool FAST = false>
 __global__ void __launch_bounds__(kBlockThreads, DF_UNI_WAVES)
 uniform_kernel(ChainArgs a) {
     using namespace uni;
@@ -368,8 +391,8 @@ uniform_kernel(ChainArgs a) {
         }
         state[smp * stride + c] = v;
     }
-    for (int i = tid; i < S; i += kBlockThreads)
-        for (int c = nd; c < stride; ++c) state[i * stride + c] = 0.f;
+    for (int i = tid; i < S; i += kBlockThreads)  // [0 | ldj_chain | ldj_elem | 1 (folded-bias input)]
+        for (int c = nd; c < stride; ++c) state[i * stride + c] = (c == nd + 3) ? 1.f : 0.f;
     __syncthreads();
 
     const int row0 = ((wave * nt) * 16 + j) * stride;  // tile tt: row0 + tt*16*stride
@@ -416,7 +439,7 @@ uniform_kernel(ChainArgs a) {
                     float ssum[kTT];
 #pragma unroll
                     for (int t = 0; t < kTT; ++t) ro[t] = row0 + (tt + t) * tstep;
-                    net_tiles<HT, kTT, OUTV, RELU, PH>(buf, N, L, tab, state, ro, ssum);
+                    net_tiles<HT, kTT, OUTV, RELU, PH, FAST>(buf, N, L, tab, state, ro, ssum);
 #pragma unroll
                     for (int t = 0; t < kTT; ++t) {
                         if (sphase) ldj_update(ro[t], sign * ssum[t], first_in_elem, last_in_elem);
@@ -491,10 +514,10 @@ uniform_kernel(ChainArgs a) {
     }
 }
 
-template <int HT, bool RELU>
+template <int HT, bool RELU, bool FAST = false>
 void* uniform_kernel_ptr_r(int mode, bool outv) {
-#define DF_U(M) (outv ? reinterpret_cast<void*>(&uniform_kernel<HT, M, true, RELU>) \
-                      : reinterpret_cast<void*>(&uniform_kernel<HT, M, false, RELU>))
+#define DF_U(M) (outv ? reinterpret_cast<void*>(&uniform_kernel<HT, M, true, RELU, FAST>) \
+                      : reinterpret_cast<void*>(&uniform_kernel<HT, M, false, RELU, FAST>))
     switch (mode) {
         case MODE_FWD: return DF_U(MODE_FWD);
         case MODE_FWD_INPLACE: return DF_U(MODE_FWD_INPLACE);
@@ -504,10 +527,12 @@ void* uniform_kernel_ptr_r(int mode, bool outv) {
 #undef DF_U
 }
 
-// variant index: bit 0 = OUTV, bit 1 = RELU
+// variant index: bit 0 = OUTV, bit 1 = RELU, bit 2 = FAST (RELU only: one first-Dense
+// k-step with the bias folded in, chain-wide)
 template <int HT>
 void* uniform_kernel_ptr(int mode, int variant) {
     const bool outv = variant & 1;
+    if (variant & 4) return uniform_kernel_ptr_r<HT, true, true>(mode, outv);
     return (variant & 2) ? uniform_kernel_ptr_r<HT, true>(mode, outv) : uniform_kernel_ptr_r<HT, false>(mode, outv);
 }
 
@@ -520,7 +545,7 @@ hipError_t launch_uniform_ht(int mode, int variant, const ChainArgs& a, unsigned
 template <int HT>
 hipError_t set_uniform_lds_limit_ht(size_t lds) {
     for (int mode = 0; mode < 4; ++mode)
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < 8; ++v) {
             hipError_t e = hipFuncSetAttribute(uniform_kernel_ptr<HT>(mode, v),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
