@@ -713,7 +713,13 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
         // Specialised-kernel descriptors when every net has the default shape.
         P.uniform = (uniform_shape && resident) ? 1 : 0;
         P.relu_only = (P.uniform && relu_only) ? 1 : 0;
-        P.fast = (P.relu_only && allow_fold && fold_all && ks1_all) ? 1 : 0;
+        bool nh1_all = true;  // every conditioner has exactly one hidden H×H Dense (n_sublayers = 2)
+        for (int li = 0; li < desc->n_layers; ++li) {
+            const df_layer_desc& L = desc->layers[li];
+            if (L.kind == DF_LAYER_NORM) continue;
+            nh1_all = nh1_all && L.n_dense_t == 3 && (L.kind != DF_LAYER_RNVP || L.n_dense_s == 3);
+        }
+        P.fast = (P.relu_only && allow_fold && fold_all && ks1_all && nh1_all) ? 1 : 0;
         if (const char* f = std::getenv("DF_NO_FAST"))
             if (f[0] == '1') P.fast = 0;
         if (uniform_shape && !resident) fail(DF_ERR_UNSUPPORTED, "internal: default-shape net split across stages");

@@ -143,7 +143,7 @@ struct Plan {
     int outv = 0;            // kernel variant: final Dense as VALU GEMV (<= 4 outputs)
     int uniform = 0;         // every layer fits the specialised kernel (ulayers valid)
     int relu_only = 0;       // specialised kernel variant: hidden σ = relu, output σ = identity
-    int fast = 0;            // specialised kernel variant: relu_only, every first Dense one k-step with its bias folded
+    int fast = 0;            // specialised kernel variant: relu_only, n_sublayers = 2, every first Dense one k-step with its bias folded
     std::vector<ULayer> ulayers;
     int samples_per_block = 0;
     int stage_max = 0;       // largest stage (bytes, multiple of kStageAlign)

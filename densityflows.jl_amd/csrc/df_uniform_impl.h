@@ -150,18 +150,20 @@ __device__ __forceinline__ void bias_act(const uint8_t* bb, int act, f32x4 (&v)[
 }
 
 // Final Dense, <= 4 outputs, as a VALU GEMV; every lane ends with all outputs.
-template <int HT, int TT, bool RELU>
+// NO > 0: the output count is a compile-time constant (FAST variant).
+template <int HT, int TT, bool RELU, int NO = 0>
 __device__ __forceinline__ void out_valu(const uint8_t* buf, const UNet& N, const f32x4 (&h)[TT][HT],
                                          f32x4 (&o)[TT]) {
     const int g = (threadIdx.x & 63) >> 4;
     const uint8_t* w3 = buf + N.off_out;
     constexpr int INP = 16 * HT;
-    const float* b3 = reinterpret_cast<const float*>(w3) + N.n_out * INP;
+    const int n_out = NO > 0 ? NO : N.n_out;
+    const float* b3 = reinterpret_cast<const float*>(w3) + n_out * INP;
 #pragma unroll
     for (int t = 0; t < TT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int oo = 0; oo < 4; ++oo) {
-        if (oo < N.n_out) {
+        if (oo < n_out) {
             float p[TT];
 #pragma unroll
             for (int t = 0; t < TT; ++t) p[t] = 0.f;
@@ -233,12 +235,14 @@ __device__ __forceinline__ float couple1(float v, float y) {
 }
 
 // Output Dense + coupling phase of net N on the last hidden activations H.
-template <int HT, int TT, bool OUTV, bool RELU, int PH>
+// NO > 0: n_out = n_af = NO at compile time (FAST variant, OUTV only).
+template <int HT, int TT, bool OUTV, bool RELU, int PH, int NO = 0>
 __device__ __forceinline__ void tail(const uint8_t* buf, const UNet& N, const ULayer& L, const int32_t* tab,
                                      float* state, const int (&ro)[TT], float (&sum)[TT], const f32x4 (&H)[TT][HT]) {
     const int g = (threadIdx.x & 63) >> 4;
     constexpr bool SPH = (PH == impl::PH_S_FWD || PH == impl::PH_S_BWD);
     const int32_t* af = tab + L.af_tab;
+    const int n_af = (OUTV && NO > 0) ? NO : L.n_af;
 #pragma unroll
     for (int t = 0; t < TT; ++t) sum[t] = 0.f;
 #ifdef DF_EXP_NOTAIL  // diagnostic build only: no output Dense / coupling (results are wrong)
@@ -255,18 +259,18 @@ __device__ __forceinline__ void tail(const uint8_t* buf, const UNet& N, const UL
 #endif
     if constexpr (OUTV) {
         f32x4 o[TT];
-        out_valu<HT, TT, RELU>(buf, N, H, o);
-        const int slot = (g < L.n_af) ? af[g] : 0;
+        out_valu<HT, TT, RELU, NO>(buf, N, H, o);
+        const int slot = (g < n_af) ? af[g] : 0;
 #pragma unroll
         for (int t = 0; t < TT; ++t) {
             const float y = impl::sel4(o[t], g);
-            if (g < L.n_af) state[ro[t] + slot] = couple1<PH>(state[ro[t] + slot], y);
+            if (g < n_af) state[ro[t] + slot] = couple1<PH>(state[ro[t] + slot], y);
             if (SPH) {
                 // ldj = Σ_k s[k] in row order (RNVP.jl:180 / :86)
                 float s_ = o[t][0];
 #pragma unroll
                 for (int oo = 1; oo < 4; ++oo)
-                    if (oo < L.n_af) s_ = s_ + o[t][oo];
+                    if (oo < n_af) s_ = s_ + o[t][oo];
                 sum[t] = s_;
             }
         }
@@ -295,7 +299,7 @@ __device__ __forceinline__ void tail(const uint8_t* buf, const UNet& N, const UL
 
 // Evaluate net N for TT 16-sample tiles (state rows ro[t]) and apply its
 // coupling phase; sum[t] = Σ_k s_k for s phases (row order).
-template <int HT, int TT, bool OUTV, bool RELU, int PH, bool FAST = false>
+template <int HT, int TT, bool OUTV, bool RELU, int PH, bool FAST = false, int NO = 0>
 __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, const ULayer& L, const int32_t* tab,
                                           float* state, const int (&ro)[TT], float (&sum)[TT]) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
@@ -315,10 +319,10 @@ __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, con
     f32x4 A[TT][HT], B[TT][HT];
     dense_first<HT, TT, KS>(buf, N, xin, A);
     bias_act<HT, TT, RELU>(buf + N.off_b0, N.act0, A, FAST ? false : !N.fold0);
-    if (N.nh == 1) {  // the default _dflt_net (n_sublayers = 2): one H×H Dense
+    if (FAST || N.nh == 1) {  // the default _dflt_net (n_sublayers = 2): one H×H Dense
         dense_hidden<HT, TT>(buf + N.off_h, A, B);
         bias_act<HT, TT, RELU>(buf + N.off_h + HT * HT * 1024, N.acth, B);
-        tail<HT, TT, OUTV, RELU, PH>(buf, N, L, tab, state, ro, sum, B);
+        tail<HT, TT, OUTV, RELU, PH, NO>(buf, N, L, tab, state, ro, sum, B);
         return;
     }
     // hidden Denses alternate A -> B -> A ... (no register copies)
@@ -333,8 +337,8 @@ __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, con
             in_a = true;
         }
     }
-    if (in_a) tail<HT, TT, OUTV, RELU, PH>(buf, N, L, tab, state, ro, sum, A);
-    else tail<HT, TT, OUTV, RELU, PH>(buf, N, L, tab, state, ro, sum, B);
+    if (in_a) tail<HT, TT, OUTV, RELU, PH, NO>(buf, N, L, tab, state, ro, sum, A);
+    else tail<HT, TT, OUTV, RELU, PH, NO>(buf, N, L, tab, state, ro, sum, B);
 }
 
 }  // namespace uni
@@ -408,7 +412,10 @@ uniform_kernel(ChainArgs a) {
 
     for (int it = 0; it < a.n_layers; ++it) {
         const int li = FWD ? it : a.n_layers - 1 - it;
-        const ULayer& L = a.ulayers[li];
+        // descriptors through the constant address space: scalar loads (the host
+        // writes them before the launch; nothing in the kernel stores to them)
+        using CULayer = const __attribute__((address_space(4))) ULayer;
+        const ULayer& L = *(const ULayer*)(&((CULayer*)(uintptr_t)a.ulayers)[li]);
         const int kind = L.kind;
         const bool first_in_elem = FWD ? L.elem_start : L.elem_end;
         const bool last_in_elem = FWD ? L.elem_end : L.elem_start;
@@ -430,21 +437,34 @@ uniform_kernel(ChainArgs a) {
         } else {
             const bool rnvp = (kind == DF_LAYER_RNVP);
             // this wave's tiles in groups of kTT (nt is a multiple of kTT)
-            auto run_net = [&](const UNet& N, auto ph_tag, bool sphase, float sign) {
+            auto tiles_loop = [&](const UNet& N, auto ph_tag, auto no_tag, bool sphase, float sign) {
                 constexpr int PH = decltype(ph_tag)::value;
-                impl::ensure_stage(N.stage, sg, a);
+                constexpr int NO = decltype(no_tag)::value;
                 const uint8_t* buf = sg.buf();
                 for (int tt = 0; tt < nt; tt += kTT) {
                     int ro[kTT];
                     float ssum[kTT];
 #pragma unroll
                     for (int t = 0; t < kTT; ++t) ro[t] = row0 + (tt + t) * tstep;
-                    net_tiles<HT, kTT, OUTV, RELU, PH, FAST>(buf, N, L, tab, state, ro, ssum);
+                    net_tiles<HT, kTT, OUTV, RELU, PH, FAST, NO>(buf, N, L, tab, state, ro, ssum);
 #pragma unroll
                     for (int t = 0; t < kTT; ++t) {
                         if (sphase) ldj_update(ro[t], sign * ssum[t], first_in_elem, last_in_elem);
                         else if (!rnvp) ldj_update(ro[t], 0.f, first_in_elem, last_in_elem);
                     }
+                }
+            };
+            auto run_net = [&](const UNet& N, auto ph_tag, bool sphase, float sign) {
+                impl::ensure_stage(N.stage, sg, a);
+                if constexpr (FAST && OUTV) {  // output count fixed per net: branch-free tails
+                    switch (N.n_out) {
+                        case 1: tiles_loop(N, ph_tag, std::integral_constant<int, 1>{}, sphase, sign); break;
+                        case 2: tiles_loop(N, ph_tag, std::integral_constant<int, 2>{}, sphase, sign); break;
+                        case 3: tiles_loop(N, ph_tag, std::integral_constant<int, 3>{}, sphase, sign); break;
+                        default: tiles_loop(N, ph_tag, std::integral_constant<int, 4>{}, sphase, sign); break;
+                    }
+                } else {
+                    tiles_loop(N, ph_tag, std::integral_constant<int, 0>{}, sphase, sign);
                 }
             };
             using PSF = std::integral_constant<int, impl::PH_S_FWD>;

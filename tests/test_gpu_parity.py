@@ -130,6 +130,29 @@ def test_forward_inplace_matches_forward(cuda):
     np.testing.assert_array_equal(_np(zz), _np(x))
 
 
+@pytest.mark.parametrize("name", ["cfg1", "cfg2"])
+def test_folded_bias_bit_identical(cuda, name, monkeypatch):
+    """The specialised kernel's FAST variant folds the first Dense's bias into the
+    last k-slot of the MFMA chain (df_plan.cpp pass 1c): fma(b, 1, W*x) rounds
+    exactly like the separate `W*x .+ b`, so x, ldj and the inverse are bitwise
+    those of the unfolded plan (DF_NO_FOLD=1) and of the non-FAST variant."""
+    spec, g, meta = G.load(name)
+    th = _t(g["theta"], cuda) if meta["n"] > 0 else None
+    outs = []
+    for env in ({}, {"DF_NO_FAST": "1"}, {"DF_NO_FOLD": "1"}):
+        for k in ("DF_NO_FAST", "DF_NO_FOLD"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        chain = spec_to_element(spec)       # fresh handle: the plan reads the env at creation
+        x, lf = dfa.forward(chain, _t(g["z"], cuda), th)
+        z, lb = dfa.backward(chain, _t(g["x_in"], cuda), th)
+        outs.append([_np(v) for v in (x, lf, z, lb)])
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("B", [0, 1, 7, 127, 128, 129, 1000, 4095])
 def test_ragged_batches(cuda, B):
     spec, g, _ = G.load("cfg1")
