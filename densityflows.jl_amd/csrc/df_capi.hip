@@ -6,6 +6,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <new>
 #include <string>
@@ -53,9 +54,14 @@ static size_t lds_for_tiles(const df_chain* c, int t) {
 // workgroup slots (time ~ rounds × (tiles + fixed per-round overhead)).
 static int choose_tiles(const df_chain* c, int mode, int64_t batch) {
     const df::Plan& P = c->plan;
-    int best = P.uniform ? df::kUniformTileGroup : 1;
+    if (const char* e = std::getenv("DF_TILES")) {  // tuning knob: force the tiles per wave
+        const int t = std::atoi(e);
+        const int step = P.uniform ? P.tile_group : 1;
+        if (t >= 1 && t <= P.tiles && t % step == 0) return t;
+    }
+    int best = P.uniform ? P.tile_group : 1;
     double best_cost = 1e300;
-    const int step = P.uniform ? df::kUniformTileGroup : 1;
+    const int step = P.uniform ? P.tile_group : 1;
     for (int t = step; t <= P.tiles; t += step) {
         const int64_t per_block = (int64_t)df::kWavesPerBlock * 16 * t;
         const int64_t nwg = (batch + per_block - 1) / per_block;
@@ -261,6 +267,14 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
     const bool wide = P.wide && !(std::getenv("DF_NO_WIDE") && std::getenv("DF_NO_WIDE")[0] == '1');
     const int tiles = wide ? df::kWideT : choose_tiles(c, mode, batch);
+    if (const char* dbg = std::getenv("DF_DEBUG_LAUNCH")) {  // tuning aid: the launch shape on stderr
+        if (dbg[0] == '1') {
+            std::fprintf(stderr, "[df] mode %d batch %lld tiles %d (max %d) occupancy:", mode, (long long)batch, tiles,
+                         P.tiles);
+            for (int t = 1; t <= P.tiles; ++t) std::fprintf(stderr, " t%d=%d", t, c->occ[mode][t]);
+            std::fprintf(stderr, "\n");
+        }
+    }
     const int64_t S = wide ? (int64_t)df::kWideWaves * 16 * df::kWideT : (int64_t)df::kWavesPerBlock * 16 * tiles;
     const int64_t grid = (batch + S - 1) / S;
     if (grid > 0x7fffffff) return set_err(DF_ERR_UNSUPPORTED, "batch too large for one launch");

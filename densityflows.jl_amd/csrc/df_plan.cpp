@@ -796,8 +796,13 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
         if (resident)
             while (P.tiles < kMaxTilesPerWave && fixed + (P.tiles + 1) * per_tile <= kLdsPerBlockTarget) ++P.tiles;
         if (P.uniform) {  // the specialised kernel evaluates tiles in groups
-            if (P.tiles < kUniformTileGroup) fail(DF_ERR_UNSUPPORTED, "LDS too small for the specialised kernel");
-            P.tiles -= P.tiles % kUniformTileGroup;
+            P.tile_group = P.fast ? kFastTileGroup : kUniformTileGroup;
+            if (P.fast && P.tiles < P.tile_group) {  // not enough LDS for a FAST tile group
+                P.fast = 0;
+                P.tile_group = kUniformTileGroup;
+            }
+            if (P.tiles < P.tile_group) fail(DF_ERR_UNSUPPORTED, "LDS too small for the specialised kernel");
+            P.tiles -= P.tiles % P.tile_group;
         }
         P.samples_per_block = kWavesPerBlock * 16 * P.tiles;
         if ((int)P.tables.size() > kMaxTableInts) fail(DF_ERR_UNSUPPORTED, "chain index tables exceed 16 KiB");

@@ -42,6 +42,10 @@ constexpr int kMaxTilesPerWave = 8;          // 16-sample tiles per wave residen
 #define DF_UNI_TT 1
 #endif
 constexpr int kUniformTileGroup = DF_UNI_TT;  // tiles the specialised kernel evaluates together
+#ifndef DF_FAST_TT
+#define DF_FAST_TT 2
+#endif
+constexpr int kFastTileGroup = DF_FAST_TT;    // ... in its FAST variant (fewer live registers per tile)
 constexpr int kLdsPerBlockTarget = DF_LDS_TARGET_KB * 1024; // two workgroups per CU
 
 enum : int32_t { IN_STATE = 0, IN_HIDDEN = 1 };
@@ -143,6 +147,7 @@ struct Plan {
     int outv = 0;            // kernel variant: final Dense as VALU GEMV (<= 4 outputs)
     int uniform = 0;         // every layer fits the specialised kernel (ulayers valid)
     int relu_only = 0;       // specialised kernel variant: hidden σ = relu, output σ = identity
+    int tile_group = 1;      // tiles per wave evaluated together (specialised kernel: 1, FAST: 2)
     int fast = 0;            // specialised kernel variant: relu_only, n_sublayers = 2, every first Dense one k-step with its bias folded
     std::vector<ULayer> ulayers;
     int samples_per_block = 0;

@@ -36,7 +36,6 @@ __device__ __forceinline__ float xgroup_sum(float p) {
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
-constexpr int kTT = kUniformTileGroup;  // 16-sample tiles evaluated together in registers
 
 // acc = W·x, x = the state features vcat(θ,z)[axis_nn] (<= 16 of them).
 // Compact fragments: [m][r < ks][lane] f32, k = 4r + lane_group.
@@ -346,9 +345,12 @@ __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, con
 #ifndef DF_UNI_WAVES
 #define DF_UNI_WAVES 4
 #endif
+#ifndef DF_FAST_WAVES
+#define DF_FAST_WAVES 4
+#endif
 
 template <int HT, int MODE, bool OUTV, bool RELU, bool FAST = false>
-__global__ void __launch_bounds__(kBlockThreads, DF_UNI_WAVES)
+__global__ void __launch_bounds__(kBlockThreads, FAST ? DF_FAST_WAVES : DF_UNI_WAVES)
 uniform_kernel(ChainArgs a) {
     using namespace uni;
     constexpr bool FWD = (MODE == MODE_FWD || MODE == MODE_FWD_INPLACE);
@@ -437,6 +439,7 @@ uniform_kernel(ChainArgs a) {
         } else {
             const bool rnvp = (kind == DF_LAYER_RNVP);
             // this wave's tiles in groups of kTT (nt is a multiple of kTT)
+            constexpr int kTT = FAST ? kFastTileGroup : kUniformTileGroup;
             auto tiles_loop = [&](const UNet& N, auto ph_tag, auto no_tag, bool sphase, float sign) {
                 constexpr int PH = decltype(ph_tag)::value;
                 constexpr int NO = decltype(no_tag)::value;
