@@ -184,6 +184,69 @@ __device__ __forceinline__ void out_valu(const uint8_t* buf, const UNet& N, cons
     }
 }
 
+// Final Dense, NO <= 4 outputs known at compile time (FAST variant), as a VALU
+// GEMV whose lane-group reduction is a transpose: two v_permlane16_swap pair up
+// outputs (0,1) and (2,3), one v_permlane32_swap completes them, so lane group g
+// ends with output g — the transformed dim it updates — instead of every lane
+// holding all outputs.  Sums associate as ((p0+p1)+(p2+p3)) over the groups,
+// bitwise xgroup_sum's order; the bias is added after the product as in out_valu.
+template <int HT, int TT, int NO>
+__device__ __forceinline__ void out_valu_t(const uint8_t* buf, const UNet& N, const f32x4 (&h)[TT][HT],
+                                           float (&y)[TT]) {
+    static_assert(NO >= 1 && NO <= 4, "FAST tails: 1..4 outputs");
+    const int g = (threadIdx.x & 63) >> 4;
+    const uint8_t* w3 = buf + N.off_out;
+    constexpr int INP = 16 * HT;
+    float p[TT][4];
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int oo = 0; oo < 4; ++oo) p[t][oo] = 0.f;
+#pragma unroll
+    for (int oo = 0; oo < NO; ++oo)
+#pragma unroll
+        for (int kq = 0; kq < HT; ++kq) {
+            const f32x4 w = lds4(w3 + ((oo * INP + 16 * kq + 4 * g) << 2));
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int t = 0; t < TT; ++t) p[t][oo] = __builtin_fmaf(w[r], h[t][kq][r], p[t][oo]);
+        }
+    const float bo = reinterpret_cast<const float*>(w3)[NO * INP + (g < NO ? g : 0)];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+        auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(p[t][0]), __float_as_uint(p[t][1]), false, false);
+        const float A = __uint_as_float(a[0]) + __uint_as_float(a[1]);  // rows: p0 g01, p1 g01, p0 g23, p1 g23
+        float Bv = 0.f;
+        if constexpr (NO > 2) {
+            auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(p[t][2]), __float_as_uint(p[t][3]), false, false);
+            Bv = __uint_as_float(b[0]) + __uint_as_float(b[1]);             // p2 g01, p3 g01, p2 g23, p3 g23
+        }
+        auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(A), __float_as_uint(Bv), false, false);
+        y[t] = (__uint_as_float(c[0]) + __uint_as_float(c[1])) + bo;      // group g: output g
+    }
+}
+
+// Lane group 0 gets (y_0 + y_1) + ... + y_{NO-1} of the per-group outputs (row order, RNVP.jl:180).
+template <int NO>
+__device__ __forceinline__ float group_row_sum(float y) {
+    float s = y;
+    if constexpr (NO > 1) {  // group 1 → group 0
+        auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(y), __float_as_uint(y), false, false);
+        s = s + __uint_as_float(a[1]);
+    }
+    if constexpr (NO > 2) {  // groups 2, 3 → groups 0, 1
+        auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(y), __float_as_uint(y), false, false);
+        const float y2 = __uint_as_float(b[1]);
+        s = s + y2;
+        if constexpr (NO > 3) {
+            auto c = __builtin_amdgcn_permlane16_swap(__float_as_uint(y2), __float_as_uint(y2), false, false);
+            s = s + __uint_as_float(c[1]);
+        }
+    }
+    return s;
+}
+
 // Final Dense through MFMA (out <= 32): rows 16m + 4g + r in out[t][m].
 template <int HT, int TT, bool RELU>
 __device__ __forceinline__ void out_mfma(const uint8_t* buf, const UNet& N, const f32x4 (&h)[TT][HT],
@@ -256,7 +319,16 @@ __device__ __forceinline__ void tail(const uint8_t* buf, const UNet& N, const UL
         return;
     }
 #endif
-    if constexpr (OUTV) {
+    if constexpr (OUTV && NO > 0) {
+        float y[TT];
+        out_valu_t<HT, TT, NO>(buf, N, H, y);
+        const int slot = af[g < NO ? g : 0];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            if (g < NO) state[ro[t] + slot] = couple1<PH>(state[ro[t] + slot], y[t]);
+            if (SPH) sum[t] = group_row_sum<NO>(y[t]);  // valid in lane group 0 (ldj_update)
+        }
+    } else if constexpr (OUTV) {
         f32x4 o[TT];
         out_valu<HT, TT, RELU, NO>(buf, N, H, o);
         const int slot = (g < n_af) ? af[g] : 0;
