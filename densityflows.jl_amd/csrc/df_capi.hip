@@ -165,7 +165,7 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
         return set_err(DF_ERR_UNSUPPORTED, "chain needs more than 160 KiB of LDS per workgroup");
     }
     if (P.wide) {
-        c->wide_lds = (size_t)2 * df::kWideStageBytes + c->tab_bytes +
+        c->wide_lds = (size_t)df::kWideBufs * df::kWideStageBytes + c->tab_bytes +
                       (size_t)df::kWideWaves * 16 * df::kWideT * P.stride * 4;
         e = df::set_wide_lds_limit(c->wide_lds);
         if (e != hipSuccess) {

@@ -114,6 +114,10 @@ struct ULayer {
 // fixed 32 KiB stages: first Dense (2 k-quads × 16 m-tiles per stage), 8 stages of
 // the hidden Dense, one stage of the output Dense ([kq < 16][m < mto]).
 constexpr int kWideStageBytes = 32 * 1024;
+#ifndef DF_WIDE_NB
+#define DF_WIDE_NB 2
+#endif
+constexpr int kWideBufs = DF_WIDE_NB;   // LDS stage ring: the DMA runs kWideBufs − 1 stages ahead
 constexpr int kWideWaves = 4;     // one wave per SIMD (512 registers each)
 constexpr int kWideT = 2;         // 16-sample tiles per wave held in registers (3 spills)
 

@@ -29,17 +29,65 @@ using impl::mfma4;
 constexpr int kThreads = kWideWaves * 64;
 constexpr int T = kWideT;
 
+// Loads through the constant address space: scalar (s_load) instead of vector
+// loads, so they never join the in-order vmcnt queue of the in-flight stage DMAs
+// (the host writes these arrays before the launch; the kernel never stores to them).
+template <class V>
+__device__ __forceinline__ const V& cref(const V* p) {
+    return *(const V*)(const __attribute__((address_space(4))) V*)(uintptr_t)p;
+}
+
+#ifndef DF_WIDE_SBIAS
+#define DF_WIDE_SBIAS 0
+#endif
+// Bias rows 16m + 4g + r of lane group g: a vector load, or (DF_WIDE_SBIAS) 16
+// scalar-loaded floats selected per lane group.
+__device__ __forceinline__ f32x4 bias4(const float* b, int m) {
+    const int g = (threadIdx.x & 63) >> 4;
+    if (!DF_WIDE_SBIAS) return *reinterpret_cast<const f32x4*>(b + 16 * m + 4 * g);
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = cref(b + 16 * m + i);
+    f32x4 r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = g == 0 ? v[q] : g == 1 ? v[4 + q] : g == 2 ? v[8 + q] : v[12 + q];
+    return r;
+}
+
 struct WStager {
     uint8_t* base;
     const int32_t* sched;
     int n;
     int idx;
     int cur;
-    __device__ __forceinline__ uint8_t* buf() const { return base + ((idx & 1) ? kWideStageBytes : 0); }
+    __device__ __forceinline__ uint8_t* buf() const { return slot(idx); }
+    __device__ __forceinline__ uint8_t* slot(int i) const { return base + (i % kWideBufs) * kWideStageBytes; }
 };
 
+// DMA instructions wave w issues for a stage of `bytes` (1 KiB per instruction,
+// chunks dealt round-robin over the waves).
+__device__ __forceinline__ int dma_ops(int bytes, int wave) {
+    const int nchunk = bytes >> 10;
+    return nchunk > wave ? (nchunk - wave + kWideWaves - 1) / kWideWaves : 0;
+}
+
+// s_waitcnt vmcnt(k) with k a run-time value (the count must be an immediate).
+__device__ __forceinline__ void wait_vmcnt(int k) {
+    switch (k) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    }
+}
+
 __device__ __forceinline__ void dma(const ChainArgs& a, int s, uint8_t* dst) {
-    const DevStage st = a.stages[s];
+    const DevStage& st = cref(a.stages + s);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint8_t* src = a.blob + st.src_off;
     const int nchunk = st.bytes >> 10;
@@ -49,15 +97,31 @@ __device__ __forceinline__ void dma(const ChainArgs& a, int s, uint8_t* dst) {
 }
 
 // Stage s, which is the next one of the fixed schedule, becomes resident; the one
-// after it is put in flight into the other buffer.
+// kWideBufs − 1 places after it is put in flight into the ring slot just freed.
+// Vector-memory loads return in order, so waiting until at most the newer
+// in-flight stages' DMA instructions of this wave are outstanding means this
+// wave's part of stage s has landed; the barrier then covers every wave's part.
 __device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
     if (s == sg.cur) return;
     const int nidx = sg.idx + 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (kWideBufs > 2) {
+        const int wave = threadIdx.x >> 6;
+        int newer = 0;
+        for (int q = 1; q < kWideBufs - 1; ++q)
+            if (nidx + q < sg.n) newer += dma_ops(cref(a.stages + cref(sg.sched + nidx + q)).bytes, wave);
+        wait_vmcnt(newer);
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // A bare s_barrier: __syncthreads()'s release fence would also wait for the
+    // newer stages' DMA (vmcnt(0)).  The stage ring is the only LDS data shared
+    // between waves here, and each wave's reads of the slot being refilled have
+    // returned (lgkmcnt(0)) before it arrives.
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     sg.idx = nidx;
     sg.cur = s;
-    if (nidx >= sg.n || sg.sched[nidx] != s) {  // off schedule (never produced by the planner)
+    if (nidx >= sg.n || cref(sg.sched + nidx) != s) {  // off schedule (never produced by the planner)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const DevStage st = a.stages[s];
         const f32x4* src = reinterpret_cast<const f32x4*>(a.blob + st.src_off);
         f32x4* dst = reinterpret_cast<f32x4*>(sg.buf());
@@ -66,7 +130,7 @@ __device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
         sg.n = 0;
         return;
     }
-    if (nidx + 1 < sg.n) dma(a, sg.sched[nidx + 1], sg.base + (((nidx + 1) & 1) ? kWideStageBytes : 0));
+    if (nidx + kWideBufs - 1 < sg.n) dma(a, cref(sg.sched + nidx + kWideBufs - 1), sg.slot(nidx + kWideBufs - 1));
 }
 
 // h = σ.(acc .+ b)  (b: 256 floats in global memory, L2-resident)
@@ -74,7 +138,7 @@ __device__ __forceinline__ void bias_act(const float* b, int act, const f32x4 (&
     const int g = (threadIdx.x & 63) >> 4;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
-        const f32x4 bb = b ? *reinterpret_cast<const f32x4*>(b + 16 * m + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 bb = b ? bias4(b, m) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             f32x4 v = acc[t][m];
@@ -211,8 +275,7 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
         if (m < N.mto) {
-            const f32x4 bb = (N.bo >= 0) ? *reinterpret_cast<const f32x4*>(a.wbias + N.bo + 16 * m + 4 * g)
-                                         : f32x4{0.f, 0.f, 0.f, 0.f};
+            const f32x4 bb = (N.bo >= 0) ? bias4(a.wbias + N.bo, m) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int t = 0; t < T; ++t) {
                 f32x4 v = out[t][m];
@@ -259,7 +322,7 @@ __global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
     constexpr bool WANT_LDJ = (MODE != MODE_FWD_INPLACE);
 
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int stage_area = 2 * kWideStageBytes;
+    const int stage_area = kWideBufs * kWideStageBytes;
     int32_t* tab = reinterpret_cast<int32_t*>(smem + stage_area);
     float* state = reinterpret_cast<float*>(smem + stage_area + a.tab_bytes);
 
@@ -278,7 +341,7 @@ __global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
     sg.n = FWD ? a.n_sched_fwd : a.n_sched_bwd;
     sg.idx = -1;
     sg.cur = -1;
-    if (sg.n > 0) dma(a, sg.sched[0], sg.base);
+    for (int q = 0; q < kWideBufs - 1 && q < sg.n; ++q) dma(a, cref(sg.sched + q), sg.slot(q));
 
     for (int i = tid; i < a.tab_ints; i += kThreads) tab[i] = a.tables[i];
     for (int i = tid; i < S * d; i += kThreads) {
@@ -319,7 +382,7 @@ __global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
 
     for (int it = 0; it < a.n_layers; ++it) {
         const int li = FWD ? it : a.n_layers - 1 - it;
-        const WLayer& L = a.wlayers[li];
+        const WLayer& L = cref(a.wlayers + li);
         const bool first_in_elem = FWD ? L.elem_start : L.elem_end;
         const bool last_in_elem = FWD ? L.elem_end : L.elem_start;
         if (L.kind == DF_LAYER_NORM) {
