@@ -37,7 +37,8 @@ PEAK_HBM_GBS = 8000.0
 # HBM bytes per launch of the headline kernel from rocprofv3 PMC counters
 # (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, WRITE_SIZE as is; KiB),
 # measured on the headline workload and committed under profiles/.
-TRAFFIC_PROFILE = os.path.join("profiles", "r01_v6_pmc_summary.txt")
+TRAFFIC_PROFILES = {"cfg2": os.path.join("profiles", "r01_v14_pmc_cfg2.txt"),
+                    "cfg4": os.path.join("profiles", "r01_v14_pmc_cfg4.txt")}
 
 
 def pmc_traffic(path):
@@ -244,9 +245,11 @@ def main():
         flop = 3.0 * info.flops_per_sample * B
         achieved_tflops = flop / kernel_s / 1e12
 
-    traffic = None
-    if args.config == "cfg2" and args.mode == "forward" and B == (1 << 20):
-        traffic = pmc_traffic(TRAFFIC_PROFILE)
+    traffic, traffic_src = None, None
+    default_b = (1 << 18) if args.config == "cfg4" else (1 << 20)
+    if args.config in TRAFFIC_PROFILES and args.mode == "forward" and B == default_b:
+        traffic_src = TRAFFIC_PROFILES[args.config]
+        traffic = pmc_traffic(traffic_src)
     if rank == 0:
         out = {
             "metric": {"forward": METRIC, "nll": "NLL (inverse+logpdf+Σ, RCCL all-reduce) Msamples/s",
@@ -271,7 +274,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": PEAK_F32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_F32_TFLOPS, 4),
                          "traffic": traffic,
-                         "traffic_source": TRAFFIC_PROFILE if traffic is not None else None,
+                         "traffic_source": traffic_src if traffic is not None else None,
                          "kernel_ms": round(kernel_s * 1e3, 4),
                          "kernel_ms_scope": "whole step (all launches)" if args.mode == "train" else "one launch",
                          "algorithmic_flop_per_sample": info.flops_per_sample,
