@@ -29,7 +29,7 @@ import DensityFlows: forward, backward, forward!, FlowElement, CouplingLayer, Co
                      FlowChain, RNVPCouplingLayer, NICECouplingLayer, NormalizationLayer
 import Flux
 
-export HIPFlowChain
+export HIPFlowChain, HIPTrainer, train_step!, trainables, copy_trainables!, hip_flow
 
 const LIB = get(ENV, "DENSITYFLOWS_HIP_LIB", joinpath(@__DIR__, "..", "libdensityflows_hip.so"))
 const ABI_VERSION = Int32(1)
@@ -238,6 +238,41 @@ function trainables(t::HIPTrainer)
     check(ccall((:df_train_get_params, LIB), Cint, (Ptr{Cvoid}, Ptr{Float32}, Int64), t.handle, p, t.n_params),
           "df_train_get_params")
     return p
+end
+
+"""
+    copy_trainables!(model::FlowChain, p::Vector{Float32})
+
+Write the device-trained flat parameters `p` (`trainables(t)`, Flux.trainables
+order) back into the Julia model, so the reference's own `save_flow` /
+`save_element` (src/Loading.jl:78-96, 124-173, 324-346) persist them.
+"""
+function copy_trainables!(model::FlowChain, p::Vector{Float32})
+    off = 0
+    for a in Flux.trainables(model)
+        n = length(a)
+        copyto!(a, 1, p, off + 1, n)
+        off += n
+    end
+    off == length(p) || throw(DimensionMismatch("model has $off trainables, device vector $(length(p))"))
+    return model
+end
+
+"""
+    hip_flow(directory; device = 0) -> Flow
+
+Weight import through the reference's own JLD2 reader: `load_flow(directory)`
+(src/Loading.jl:348-377) rebuilds the Flow that `save_flow` wrote, then its
+model is wrapped as `FlowChain((HIPFlowChain(model),))` (src/Chains.jl:78-80),
+so `logpdf`, `sample` and the @flow_wrapper methods of the returned Flow run on
+the MI355X.  Metadata, base distribution and loss histories are kept.
+"""
+function hip_flow(directory::AbstractString; device::Integer = 0)
+    f = DensityFlows.load_flow(directory)
+    hip = FlowChain((HIPFlowChain(f.model; device = device),))
+    T = eltype(f.metadata.θ_min)
+    return DensityFlows.Flow{T, f.metadata.d, f.metadata.n, typeof(hip), typeof(f.base), typeof(f.metadata.θ_min)}(
+        hip, f.base, f.metadata, f.train_loss, f.valid_loss)
 end
 
 end # module
