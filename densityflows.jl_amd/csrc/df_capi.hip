@@ -269,8 +269,9 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     const int tiles = wide ? df::kWideT : choose_tiles(c, mode, batch);
     if (const char* dbg = std::getenv("DF_DEBUG_LAUNCH")) {  // tuning aid: the launch shape on stderr
         if (dbg[0] == '1') {
-            std::fprintf(stderr, "[df] mode %d batch %lld tiles %d (max %d) occupancy:", mode, (long long)batch, tiles,
-                         P.tiles);
+            std::fprintf(stderr, "[df] mode %d batch %lld kernel %s tiles %d (max %d) occupancy:", mode,
+                         (long long)batch,
+                         wide ? "wide" : !P.uniform ? "generic" : P.fast ? "uniform-fast" : "uniform", tiles, P.tiles);
             for (int t = 1; t <= P.tiles; ++t) std::fprintf(stderr, " t%d=%d", t, c->occ[mode][t]);
             std::fprintf(stderr, "\n");
         }

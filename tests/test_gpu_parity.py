@@ -153,6 +153,68 @@ def test_folded_bias_bit_identical(cuda, name, monkeypatch):
             np.testing.assert_array_equal(a, b)
 
 
+def _fast_case_chain(case, rng):
+    """Default-shape relu chains that take the specialised kernel's FAST variant
+    with 1, 2, 3 and 4 transformed dims per layer, NICE layers, conditioning and
+    every hidden width the variant has (16, 32, 64)."""
+    L = dfa.CouplingLayer
+    if case == "af1_h64":      # d=4: n_af 1 (in 3), then 3 (in 1)
+        return 4, 0, dfa.FlowChain(L(4, [2], hidden_dim=64, rng=rng), L(4, [1, 3, 4], hidden_dim=64, rng=rng))
+    if case == "af4_h64":      # d=6: n_af 4 (in 2) twice
+        return 6, 0, dfa.FlowChain(L(6, [1, 2, 3, 4], hidden_dim=64, rng=rng),
+                                   L(6, [6, 2, 5, 3], hidden_dim=64, rng=rng))
+    if case == "in4_h64":      # d=6: n_af 4 (in 2, folded), then 2 (in 4: no free k-slot) → FAST off
+        return 6, 0, dfa.FlowChain(L(6, [1, 2, 3, 4], hidden_dim=64, rng=rng),
+                                   L(6, [6, 2], hidden_dim=64, rng=rng))
+    if case == "nice_h32":     # NICE + RNVP, conditioned (n=1), hidden 32
+        return 5, 1, dfa.FlowChain(L(dfa.NICECouplingLayer, 5, [1, 2, 3], n=1, hidden_dim=32, rng=rng),
+                                   L(5, [3, 4, 5], n=1, hidden_dim=32, rng=rng),
+                                   L(dfa.NICECouplingLayer, 5, [5, 1, 2], n=1, hidden_dim=32, rng=rng))
+    if case == "block_h16":    # CouplingBlocks, hidden 16
+        return 5, 0, dfa.FlowChain.repeat(dfa.CouplingBlock, 2, 5, hidden_dim_s=16, hidden_dim_t=16, rng=rng)
+    raise ValueError(case)
+
+
+@pytest.mark.parametrize("case", ["af1_h64", "af4_h64", "in4_h64", "nice_h32", "block_h16"])
+def test_fast_variant_cases(cuda, case, monkeypatch, capfd):
+    """FAST-variant tails for every output count: against the fp64 oracle, and
+    bitwise against the non-FAST / unfolded plans of the same chain."""
+    import bench
+
+    outs = []
+    for env in ({"DF_DEBUG_LAUNCH": "1"}, {"DF_NO_FAST": "1"}, {"DF_NO_FOLD": "1"}):
+        for k in ("DF_NO_FAST", "DF_NO_FOLD", "DF_DEBUG_LAUNCH"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        rng = np.random.default_rng(11)
+        d, n, chain = _fast_case_chain(case, rng)
+        bench._init_nets(chain, rng)      # non-zero biases: the folded slot carries them
+        rz = np.random.default_rng(12)
+        B = 3000
+        z = rz.standard_normal((d, B)).astype(np.float32)
+        th = rz.random((n, B)).astype(np.float32) if n else None
+        tth = _t(th, cuda) if n else None
+        x, lf = dfa.forward(chain, _t(z, cuda), tth)
+        zb, lb = dfa.backward(chain, x, tth)
+        outs.append([_np(v) for v in (x, lf, zb, lb)])
+        if "DF_DEBUG_LAUNCH" in env:
+            import torch
+
+            torch.cuda.synchronize()
+            launches = capfd.readouterr().err
+            want = "kernel uniform " if case == "in4_h64" else "kernel uniform-fast "
+            assert want in launches, launches
+            xo, lo = O.forward(chain.to_spec(), z, th if n else np.zeros((0, B), np.float32), np.float64)
+            assert close(_np(x), xo, RTOL)[0] and close(_np(lf), lo, RTOL)[0]
+            # chain round trip: the inverse re-derives s from recomputed inputs, so the
+            # cancellation is to rounding (runtests.jl:93 uses atol = 2f-6), not exact
+            assert np.all(np.abs(_np(lf) + _np(lb)) <= 2e-6 + 1e-5 * np.abs(_np(lf)))
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("B", [0, 1, 7, 127, 128, 129, 1000, 4095])
 def test_ragged_batches(cuda, B):
     spec, g, _ = G.load("cfg1")
