@@ -199,14 +199,6 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
         }
     }
     bias_act(N.b0 >= 0 ? a.wbias + N.b0 : nullptr, N.act0, acc, h);
-    if (hs) {
-#pragma unroll
-        for (int t = 0; t < T; ++t)
-            if (gs[t] >= 0)
-#pragma unroll
-                for (int m = 0; m < 16; ++m)
-                    *reinterpret_cast<f32x4*>(hs + gs[t] * a.hsave_w + 16 * m + 4 * g) = h[t][m];
-    }
 
     // ---- hidden Dense 256×256: 8 stages of 2 k-quads ----
 #pragma unroll
@@ -216,6 +208,15 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
         ensure(N.stage0 + N.nst0 + st, sg, a);
+        if (hs && st == 0) {  // training: keep H0.  Stored after the stage switch, so the
+                              // stores drain under this stage's MFMAs, not at its vmcnt(0)
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+                if (gs[t] >= 0)
+#pragma unroll
+                    for (int m = 0; m < 16; ++m)
+                        *reinterpret_cast<f32x4*>(hs + gs[t] * a.hsave_w + 16 * m + 4 * g) = h[t][m];
+        }
         const uint8_t* buf = sg.buf() + lane * 16;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
@@ -235,7 +236,10 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
         }
     }
     bias_act(N.b1 >= 0 ? a.wbias + N.b1 : nullptr, N.act1, acc, h);
-    if (hs) {
+
+    // ---- output Dense (<= 32 outputs): [kq < 16][m < mto] ----
+    ensure(N.stage0 + N.nst0 + 8, sg, a);
+    if (hs) {  // training: keep H1 (after the stage switch, as H0)
         float* hs1 = hs + a.batch * a.hsave_w;
 #pragma unroll
         for (int t = 0; t < T; ++t)
@@ -244,9 +248,6 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
                 for (int m = 0; m < 16; ++m)
                     *reinterpret_cast<f32x4*>(hs1 + gs[t] * a.hsave_w + 16 * m + 4 * g) = h[t][m];
     }
-
-    // ---- output Dense (<= 32 outputs): [kq < 16][m < mto] ----
-    ensure(N.stage0 + N.nst0 + 8, sg, a);
     const uint8_t* buf = sg.buf() + lane * 16;
 #pragma unroll
     for (int t = 0; t < T; ++t) out[t][0] = out[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
