@@ -159,10 +159,8 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
     f32x4 h[T][16], acc[T][16];
 
     // ---- first Dense: features vcat(θ, z)[axis_nn] from the LDS state, k = 4s + g ----
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-        for (int m = 0; m < 16; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // (the first k-step, which always exists, starts every chain from an inline 0:
+    // no accumulator zeroing)
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
         if (st < N.nst0) {
@@ -192,7 +190,10 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
                                 for (int mm = 0; mm < 4; ++mm)
 #pragma unroll
                                     for (int t = 0; t < T; ++t)
-                                        acc[t][m0 + mm] = mfma4(w[mm][r], xin[t][r], acc[t][m0 + mm]);
+                                        acc[t][m0 + mm] = mfma4(w[mm][r], xin[t][r],
+                                                                (st == 0 && kk == 0 && r == 0)
+                                                                    ? f32x4{0.f, 0.f, 0.f, 0.f}
+                                                                    : acc[t][m0 + mm]);
                     }
                 }
             }
@@ -200,11 +201,7 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
     }
     bias_act(N.b0 >= 0 ? a.wbias + N.b0 : nullptr, N.act0, acc, h);
 
-    // ---- hidden Dense 256×256: 8 stages of 2 k-quads ----
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-        for (int m = 0; m < 16; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // ---- hidden Dense 256×256: 8 stages of 2 k-quads (chains start from an inline 0) ----
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
         ensure(N.stage0 + N.nst0 + st, sg, a);
@@ -231,7 +228,10 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
 #pragma unroll
                     for (int mm = 0; mm < 4; ++mm)
 #pragma unroll
-                        for (int t = 0; t < T; ++t) acc[t][m0 + mm] = mfma4(w[mm][r], h[t][kq][r], acc[t][m0 + mm]);
+                        for (int t = 0; t < T; ++t)
+                            acc[t][m0 + mm] = mfma4(w[mm][r], h[t][kq][r],
+                                                    (st == 0 && kk == 0 && r == 0) ? f32x4{0.f, 0.f, 0.f, 0.f}
+                                                                                   : acc[t][m0 + mm]);
             }
         }
     }
