@@ -144,6 +144,8 @@ def main():
                     help="cfg2 is the headline (BASELINE configs[1]); cfg1/cfg4 are secondary measurements")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="train mode, one rank: replay each step as one hipGraph (df_train_step_graph)")
     args = ap.parse_args()
 
     import torch
@@ -196,6 +198,9 @@ def main():
         gview = trainer.grad() if dist is not None else None
 
         def step():
+            if args.graph and dist is None:
+                trainer.step_graph(xbuf, thbuf, B, B, s64[:1])
+                return
             trainer.gradient(xbuf, thbuf, B, B * world, s64[:1])
             if dist is not None:
                 dist.all_reduce(gview)

@@ -121,6 +121,7 @@ SIGNATURES = {
     "df_train_grad_ptr": (C.c_int, [_VP, C.POINTER(_VP)]),
     "df_train_apply": (C.c_int, [_VP, _VP]),
     "df_train_step": (C.c_int, [_VP, _VP, _VP, _I64, _VP, _VP]),
+    "df_train_step_graph": (C.c_int, [_VP, _VP, _VP, _I64, _I64, _VP, _VP]),
     "df_train_get_params": (C.c_int, [_VP, _FP, _I64]),
     "df_train_set_params": (C.c_int, [_VP, _FP, _I64]),
     "df_device_alloc": (C.c_int, [C.POINTER(_VP), C.c_size_t]),

@@ -286,6 +286,7 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
         hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->d_partial), sizeof(double) * grid);
         if (e != hipSuccess) return set_err(DF_ERR_NOMEM, "hipMalloc failed (NLL partials)");
         c->partial_cap = grid;
+        c->partial_gen++;
     }
 
     df::ChainArgs a{};

@@ -26,6 +26,7 @@ struct df_chain {
     bool has_bounds = false;
     double* d_partial = nullptr;
     int64_t partial_cap = 0;
+    int64_t partial_gen = 0;  // bumped when d_partial is reallocated (captured train graphs hold it)
     int stage_bytes = 0;
     int n_stage_bufs = 1;
     void* d_sched = nullptr;    // [fwd schedule | bwd schedule]

@@ -74,8 +74,9 @@ hipError_t launch_scale(float* dst, const float* src, float s, int64_t count, hi
 hipError_t launch_norm_adjoint(float* zbar, const float* xmin, const float* xmax, float alpha, float beta, int d,
                                int64_t batch, hipStream_t st);
 hipError_t launch_reduce_grads(const float* partial, int n_parts, int64_t p_total, float* grad, hipStream_t st);
+// Adam update with βᵗ read from bt[0..1] on the device, then βᵗ .*= β (one more launch).
 hipError_t launch_adam(float* x, const float* g, float* m, float* v, int64_t count, float eta, float b1, float b2,
-                       float eps, float bt1, float bt2, hipStream_t st);
+                       float eps, float* bt, hipStream_t st);
 hipError_t launch_repack(float* blob, const int32_t* dst, const int32_t* src, int64_t count, const float* params,
                          hipStream_t st);
 

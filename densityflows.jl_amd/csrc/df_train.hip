@@ -50,10 +50,13 @@ __global__ void reduce_grads_kernel(const float* partial, int n_parts, int64_t p
 // Optimisers.Adam (apply!, Optimisers.jl v0.4):
 //   m = β1 m + (1-β1) g;  v = β2 v + (1-β2) g²
 //   x -= m / (1-β1ᵗ) / (sqrt(v / (1-β2ᵗ)) + ϵ) · η          (all Float32)
+// βᵗ lives on the device (bt[0], bt[1]) so that a captured train step (hipGraph)
+// replays with the current power; adam_advance_kernel moves it on after the update.
 __global__ void adam_kernel(float* x, const float* g, float* m, float* v, int64_t count, float eta, float b1,
-                            float b2, float eps, float bt1, float bt2) {
+                            float b2, float eps, const float* bt) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
+    const float bt1 = bt[0], bt2 = bt[1];
     const float gi = g[i];
     const float mi = b1 * m[i] + (1.f - b1) * gi;
     const float vi = b2 * v[i] + (1.f - b2) * (gi * gi);
@@ -61,6 +64,13 @@ __global__ void adam_kernel(float* x, const float* g, float* m, float* v, int64_
     v[i] = vi;
     const float upd = mi / (1.f - bt1) / (sqrtf(vi / (1.f - bt2)) + eps) * eta;
     x[i] = x[i] - upd;
+}
+
+__global__ void adam_advance_kernel(float* bt, float b1, float b2) {
+    if (threadIdx.x == 0) {
+        bt[0] = bt[0] * b1;  // βᵗ .* β in Float32 (Optimisers.Adam)
+        bt[1] = bt[1] * b2;
+    }
 }
 
 __global__ void repack_kernel(float* blob, const int32_t* dst, const int32_t* src, int64_t count,
@@ -127,10 +137,11 @@ hipError_t launch_reduce_grads(const float* partial, int n_parts, int64_t p_tota
 }
 
 hipError_t launch_adam(float* x, const float* g, float* m, float* v, int64_t count, float eta, float b1, float b2,
-                       float eps, float bt1, float bt2, hipStream_t st) {
-    if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(count, 256)), dim3(256), 0, st, x, g, m, v, count, eta, b1, b2,
-                       eps, bt1, bt2);
+                       float eps, float* bt, hipStream_t st) {
+    if (count > 0)
+        hipLaunchKernelGGL(adam_kernel, dim3(blocks_for(count, 256)), dim3(256), 0, st, x, g, m, v, count, eta, b1, b2,
+                           eps, static_cast<const float*>(bt));
+    hipLaunchKernelGGL(adam_advance_kernel, dim3(1), dim3(64), 0, st, bt, b1, b2);
     return hipGetLastError();
 }
 

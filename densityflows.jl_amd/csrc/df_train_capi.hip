@@ -58,10 +58,26 @@ bool act_trainable(int a) {
 
 }  // namespace
 
+// One captured train step (df_train_step_graph): valid while the buffers it
+// names are the ones it was captured with.
+struct TrainGraph {
+    const void* x = nullptr;
+    const void* theta = nullptr;
+    const void* lp = nullptr;
+    int64_t batch = 0, n_total = 0, cap_gen = -1, partial_gen = -1;
+    int seen = 0;                     // eager runs with this key (captured on the second)
+    hipGraphExec_t exec = nullptr;
+    uint64_t last_use = 0;
+};
+
 struct df_train {
     df_chain* c = nullptr;
     df_adam opt{};
-    float bt1 = 0.f, bt2 = 0.f;  // βᵗ of the next update
+    float* d_bt = nullptr;            // device βᵗ of the next update (Adam), [β1ᵗ, β2ᵗ]
+    int64_t cap_gen = 0;              // bumped when the batch-sized buffers are reallocated
+    hipStream_t cap_stream = nullptr; // capture stream of df_train_step_graph
+    std::vector<TrainGraph> graphs;
+    uint64_t use_clock = 0;
     int64_t P = 0;
     int relu = 0;
     std::vector<GNet> nets;
@@ -113,7 +129,18 @@ struct df_train {
 
 namespace {
 
+void drop_graphs(df_train* t) {
+    for (TrainGraph& g : t->graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    t->graphs.clear();
+}
+
 void free_all(df_train* t) {
+    drop_graphs(t);
+    if (t->cap_stream) (void)hipStreamDestroy(t->cap_stream);
+    t->cap_stream = nullptr;
+    if (t->d_bt) (void)hipFree(t->d_bt);
+    t->d_bt = nullptr;
     void* ptrs[] = {t->d_params, t->d_m,    t->d_v,    t->d_grad, t->d_partial, t->d_tblob, t->d_pdst,
                     t->d_psrc,   t->d_tdst, t->d_tsrc, t->d_snap, t->d_zbar,    t->d_ebuf,  t->d_lpsum,
                     t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_ly,   t->d_lx,      t->d_hsave,
@@ -318,6 +345,7 @@ int build_nets(df_train* t) {
 
 int ensure_capacity(df_train* t, int64_t batch) {
     if (batch <= t->cap) return DF_OK;
+    t->cap_gen++;  // captured train steps name the old buffers
     const Plan& P = t->c->plan;
     for (float** p : {&t->d_snap, &t->d_zbar, &t->d_ebuf})
         if (*p) {
@@ -590,8 +618,6 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
         delete t;
         return set_err(DF_ERR_INVALID, "invalid Adam hyper-parameters");
     }
-    t->bt1 = t->opt.beta1;
-    t->bt2 = t->opt.beta2;
     const Plan& P = c->plan;
     t->P = (int64_t)P.trainables.size();
     t->relu = P.relu_only;
@@ -652,9 +678,17 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
         hipMalloc(reinterpret_cast<void**>(&t->d_v), pb) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&t->d_grad), pb) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&t->d_partial), pb * t->grid) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&t->d_lpsum), sizeof(double)) != hipSuccess) {
+        hipMalloc(reinterpret_cast<void**>(&t->d_lpsum), sizeof(double)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&t->d_bt), 2 * sizeof(float)) != hipSuccess) {
         df_train_destroy(t);
         return set_err(DF_ERR_NOMEM, "hipMalloc failed (training state)");
+    }
+    {  // Optimisers.setup: βᵗ = β for the first update
+        const float bt[2] = {t->opt.beta1, t->opt.beta2};
+        if (hipMemcpy(t->d_bt, bt, sizeof(bt), hipMemcpyHostToDevice) != hipSuccess) {
+            df_train_destroy(t);
+            return set_err(DF_ERR_HIP, "hipMemcpy(Adam state)");
+        }
     }
     if ((rc = upload(t->tblob, &t->d_tblob)) != DF_OK || (rc = upload(t->lblob, &t->d_lblob)) != DF_OK ||
         (rc = upload(t->ldst, &t->d_ldst)) != DF_OK || (rc = upload(t->lsrc, &t->d_lsrc)) != DF_OK ||
@@ -774,10 +808,8 @@ int df_train_apply(df_train* t, void* stream) {
     DeviceGuard gd(t->c->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipError_t e = launch_adam(t->d_params, t->d_grad, t->d_m, t->d_v, t->P, t->opt.eta, t->opt.beta1,
-                               t->opt.beta2, t->opt.epsilon, t->bt1, t->bt2, st);
+                               t->opt.beta2, t->opt.epsilon, t->d_bt, st);
     if (e != hipSuccess) return hip_err(e, "Adam kernel launch");
-    t->bt1 = t->bt1 * t->opt.beta1;  // βᵗ .* β in Float32
-    t->bt2 = t->bt2 * t->opt.beta2;
     return repack(t, st);
 }
 
@@ -787,6 +819,83 @@ int df_train_step(df_train* t, const float* x, const float* theta_raw, int64_t b
     if (batch == 0) return DF_OK;
     int rc = df_train_gradient(t, x, theta_raw, batch, batch, logpdf_sum, stream);
     return rc != DF_OK ? rc : df_train_apply(t, stream);
+}
+
+int df_train_step_graph(df_train* t, const float* x, const float* theta_raw, int64_t batch, int64_t n_total,
+                        double* logpdf_sum, void* stream) {
+    if (!t) return set_err(DF_ERR_INVALID, "null trainer");
+    if (batch == 0) return DF_OK;
+    if (batch < 0) return set_err(DF_ERR_SHAPE, "negative batch size");
+    if (n_total < batch) return set_err(DF_ERR_INVALID, "n_total must be >= batch and >= 1");
+    DeviceGuard gd(t->c->device);
+    if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint64_t now = ++t->use_clock;
+    TrainGraph* g = nullptr;
+    for (TrainGraph& e : t->graphs)
+        if (e.x == x && e.theta == theta_raw && e.lp == logpdf_sum && e.batch == batch && e.n_total == n_total) g = &e;
+    if (g && (g->cap_gen != t->cap_gen || g->partial_gen != t->c->partial_gen)) {  // stale buffers
+        if (g->exec) (void)hipGraphExecDestroy(g->exec);
+        g->exec = nullptr;
+        g->seen = 0;
+    }
+    if (g && g->exec) {  // replay
+        g->last_use = now;
+        hipError_t e = hipGraphLaunch(g->exec, st);
+        return e == hipSuccess ? DF_OK : hip_err(e, "hipGraphLaunch(train step)");
+    }
+    if (!g || g->seen == 0) {  // first sight of this key: eager (allocates every buffer it needs)
+        if (!g) {
+            if (t->graphs.size() >= 4) {  // keep the 4 most recently used keys
+                auto lru = t->graphs.begin();
+                for (auto it = t->graphs.begin(); it != t->graphs.end(); ++it)
+                    if (it->last_use < lru->last_use) lru = it;
+                if (lru->exec) (void)hipGraphExecDestroy(lru->exec);
+                t->graphs.erase(lru);
+            }
+            TrainGraph ng;
+            ng.x = x;
+            ng.theta = theta_raw;
+            ng.lp = logpdf_sum;
+            ng.batch = batch;
+            ng.n_total = n_total;
+            t->graphs.push_back(ng);
+            g = &t->graphs.back();
+        }
+        int rc = df_train_gradient(t, x, theta_raw, batch, n_total, logpdf_sum, stream);
+        if (rc == DF_OK) rc = df_train_apply(t, stream);
+        g->seen = 1;
+        g->cap_gen = t->cap_gen;
+        g->partial_gen = t->c->partial_gen;
+        g->last_use = now;
+        return rc;
+    }
+    // second sight: capture gradient + Adam + repack on a private stream, then replay
+    if (!t->cap_stream && hipStreamCreateWithFlags(&t->cap_stream, hipStreamNonBlocking) != hipSuccess)
+        return set_err(DF_ERR_HIP, "hipStreamCreate failed");
+    hipError_t e = hipStreamBeginCapture(t->cap_stream, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) return hip_err(e, "hipStreamBeginCapture");
+    int rc = df_train_gradient(t, x, theta_raw, batch, n_total, logpdf_sum, t->cap_stream);
+    if (rc == DF_OK) rc = df_train_apply(t, t->cap_stream);
+    hipGraph_t graph = nullptr;
+    e = hipStreamEndCapture(t->cap_stream, &graph);
+    if (rc != DF_OK || e != hipSuccess || !graph) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc != DF_OK ? rc : hip_err(e, "hipStreamEndCapture");
+    }
+    if (g->cap_gen != t->cap_gen || g->partial_gen != t->c->partial_gen) {  // a buffer moved while capturing
+        (void)hipGraphDestroy(graph);
+        return set_err(DF_ERR_HIP, "internal: training buffers reallocated during graph capture");
+    }
+    e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) {
+        g->exec = nullptr;
+        return hip_err(e, "hipGraphInstantiate(train step)");
+    }
+    g->last_use = now;
+    e = hipGraphLaunch(g->exec, st);
+    return e == hipSuccess ? DF_OK : hip_err(e, "hipGraphLaunch(train step)");
 }
 
 int df_train_get_params(df_train* t, float* host_out, int64_t count) {

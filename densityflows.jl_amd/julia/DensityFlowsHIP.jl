@@ -29,7 +29,7 @@ import DensityFlows: forward, backward, forward!, FlowElement, CouplingLayer, Co
                      FlowChain, RNVPCouplingLayer, NICECouplingLayer, NormalizationLayer
 import Flux
 
-export HIPFlowChain, HIPTrainer, train_step!, trainables, copy_trainables!, hip_flow
+export HIPFlowChain, HIPTrainer, train_step!, train_step_graph!, trainables, copy_trainables!, hip_flow
 
 const LIB = get(ENV, "DENSITYFLOWS_HIP_LIB", joinpath(@__DIR__, "..", "libdensityflows_hip.so"))
 const ABI_VERSION = Int32(1)
@@ -229,6 +229,20 @@ function train_step!(t::HIPTrainer, x::Array{Float32,N}, θ::Array{Float32,N}) w
     finally
         foreach(_free, (dx, dθ))
     end
+    return nothing
+end
+
+"""
+    train_step_graph!(t, x_dev, θ_dev, B)
+
+train_step! on device buffers that stay the same across the mini-batch loop
+(copy each batch into them): the step is captured as one hipGraph the second
+time the buffers repeat and replayed afterwards (df_train_step_graph).
+"""
+function train_step_graph!(t::HIPTrainer, x::Ptr{Float32}, θ::Ptr{Float32}, B::Integer; stream = C_NULL)
+    check(ccall((:df_train_step_graph, LIB), Cint,
+                (Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32}, Int64, Int64, Ptr{Cvoid}, Ptr{Cvoid}),
+                t.handle, x, θ, B, B, C_NULL, stream), "df_train_step_graph")
     return nothing
 end
 

@@ -97,6 +97,14 @@ class HIPTrainer:
         _lib.check(self.lib.df_train_step(self.handle, _ptr(xbuf), _ptr(thbuf), C.c_int64(batch), _ptr(lpsum),
                                           _stream(self.device)), "df_train_step")
 
+    def step_graph(self, xbuf, thbuf, batch: int, n_total: int = None, lpsum=None):
+        """gradient + apply replayed as one hipGraph once the same buffers repeat
+        (df_train_step_graph); pass persistent staging buffers."""
+        n_total = batch if n_total is None else n_total
+        _lib.check(self.lib.df_train_step_graph(self.handle, _ptr(xbuf), _ptr(thbuf), C.c_int64(batch),
+                                                C.c_int64(n_total), _ptr(lpsum), _stream(self.device)),
+                   "df_train_step_graph")
+
     def get_params(self) -> np.ndarray:
         out = np.empty(self.num_params, dtype=np.float32)
         _lib.check(self.lib.df_train_get_params(self.handle, out.ctypes.data_as(C.POINTER(C.c_float)),
@@ -190,7 +198,7 @@ def _loss(flow, x, th, group=None):
 
 
 def train_(flow, data, state: TrainState, epochs: int = 100, batchsize: int = 64, shuffle: bool = True,
-           verbose: bool = True, rng=None, group=None):
+           verbose: bool = True, rng=None, group=None, graphs: bool = True):
     """``train!(flow, data, opt_state; epochs, batchsize, shuffle, verbose)`` — src/Flows.jl:380-445.
 
     Per epoch: mini-batches of the training split (Flux.DataLoader: reshuffled
@@ -199,7 +207,11 @@ def train_(flow, data, state: TrainState, epochs: int = 100, batchsize: int = 64
     ``flow.train_loss`` / ``flow.valid_loss``.  θ is normalised with the
     Flow's MetaData inside the kernels (= normalized_training_data, Data.jl:189).
     Under torch.distributed every batch is sharded over the ranks and the
-    gradient all-reduced (every rank must pass the same ``rng`` seed)."""
+    gradient all-reduced (every rank must pass the same ``rng`` seed).
+    On one device each mini-batch is gathered into a persistent staging buffer
+    and the step (reverse sweep, reduction, Adam, repack) is replayed as one
+    hipGraph (``graphs``; df_train_step_graph), which removes the per-launch
+    host overhead that dominates the reference's default batchsize of 64."""
     import torch
 
     from .parallel import shard_range
@@ -217,6 +229,7 @@ def train_(flow, data, state: TrainState, epochs: int = 100, batchsize: int = 64
     Ts = tt.view(N, n) if tt is not None else None
     dist = _dist()
     rank, world = (dist.get_rank(group), dist.get_world_size(group)) if dist is not None else (0, 1)
+    staging = {}  # batch size → persistent (x, θ) device buffers (stable pointers for the graphs)
     for _ in range(epochs):
         order = rng.permutation(N) if shuffle else np.arange(N)
         for b0 in range(0, N, batchsize):
@@ -224,6 +237,16 @@ def train_(flow, data, state: TrainState, epochs: int = 100, batchsize: int = 64
             B = idx.shape[0]
             a, b = shard_range(B, rank, world)
             ii = torch.as_tensor(idx[a:b], device=dev)
+            if dist is None and graphs:
+                if B not in staging:
+                    staging[B] = (torch.empty((B, flow.d), dtype=Xs.dtype, device=dev),
+                                  torch.empty((B, n), dtype=Ts.dtype, device=dev) if Ts is not None else None)
+                xb, tb = staging[B]
+                torch.index_select(Xs, 0, ii, out=xb)
+                if Ts is not None:
+                    torch.index_select(Ts, 0, ii, out=tb)
+                tr.step_graph(xb, tb, B)
+                continue
             xb = Xs.index_select(0, ii).contiguous()
             tb = Ts.index_select(0, ii).contiguous() if Ts is not None else None
             if dist is None:

@@ -233,6 +233,16 @@ int df_train_apply(df_train* t, void* stream);
 /* df_train_gradient (n_total = batch) followed by df_train_apply. */
 int df_train_step(df_train* t, const float* x, const float* theta_raw, int64_t batch, double* logpdf_sum,
                   void* stream);
+/* df_train_gradient (mean over n_total) + df_train_apply as ONE hipGraph
+ * launch: the reverse sweep's per-net kernels, reduction, Adam and repack
+ * are captured the second time the same (x, θ, batch, n_total, logpdf_sum)
+ * buffers are seen and replayed from then on (the first call runs eagerly).
+ * For train!'s mini-batch loop (src/Flows.jl:396-414) with reused device
+ * staging buffers, where per-launch overhead dominates small batches.
+ * Captures are dropped when a buffer they name is reallocated.  Not for
+ * data parallelism (the gradient all-reduce sits between the two halves). */
+int df_train_step_graph(df_train* t, const float* x, const float* theta_raw, int64_t batch, int64_t n_total,
+                        double* logpdf_sum, void* stream);
 /* Copy the current trainables to / from host memory (count floats). */
 int df_train_get_params(df_train* t, float* host_out, int64_t count);
 int df_train_set_params(df_train* t, const float* host_in, int64_t count);

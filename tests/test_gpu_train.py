@@ -396,3 +396,57 @@ def test_gradient_parity_edge_cases(cuda, path, name, B):
     """NICE-only chains between NormalizationLayers, Denses without bias,
     unconditional 2-d chains, and batches around the 16-sample tile."""
     test_gradient_parity(cuda, path, name, B)
+
+
+@pytest.mark.parametrize("name", ["readme", "cfg2", "mixed"])
+def test_step_graph_matches_eager_steps(cuda, path, name):
+    """df_train_step_graph (eager on first sight of its buffers, captured on the
+    second, replayed after) leaves bitwise the parameters of the same sequence of
+    eager df_train_step calls: same kernels, Adam's βᵗ advanced on the device.
+    The sequence changes batch size (a new graph), grows the batch past the
+    trainer's capacity (buffers reallocated: the old capture is dropped) and
+    comes back to the first buffers."""
+    import torch
+
+    spec, chain, d, n = _setup(name, seed=7)
+    chain2 = spec_to_element(spec)    # a trainer repacks its chain's weights: one chain each
+    eager = HIPTrainer(chain.hip(device=cuda.index or 0), Adam(1e-3))
+    graph = HIPTrainer(chain2.hip(device=cuda.index or 0), Adam(1e-3))
+    bufs = {}
+    for B in (64, 64, 64, 64, 33, 33, 33, 64, 5000, 5000, 5000, 64, 64):
+        x, th = _inputs(d, n, B, seed=B)
+        xd, td = _dev(x, cuda), (_dev(th, cuda) if n else None)
+        if B not in bufs:                       # persistent staging buffers per batch size
+            bufs[B] = (torch.empty_like(xd), torch.empty_like(td) if n else None)
+        xs, ts = bufs[B]
+        xs.copy_(xd)
+        if n:
+            ts.copy_(td)
+        eager.step(xd, td, B)
+        graph.step_graph(xs, ts, B)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(graph.get_params(), eager.get_params())
+
+
+def test_train_graphs_match_eager(cuda):
+    """train_ with the graph-replayed steps (default) equals train_ with eager steps, bitwise."""
+    import os
+
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    x = np.load(os.path.join(here, "datatest_x.npy"))
+    th = np.load(os.path.join(here, "datatest_theta.npy"))
+    out = []
+    for graphs in (True, False):
+        rng = np.random.default_rng(0)
+        data = dfa.DataArrays(x, th, rng=rng)
+        chain = dfa.FlowChain(
+            dfa.CouplingLayer(data, [1, 2, 3], hidden_dim_s=16, hidden_dim_t=16, rng=rng),
+            dfa.CouplingLayer(data, [3, 4, 5], hidden_dim_s=16, hidden_dim_t=16, rng=rng),
+            dfa.NormalizationLayer.from_data(x, -1.0, 1.0))
+        flow = dfa.Flow(chain, data)
+        state = setup(Adam(1e-3), flow)
+        train_(flow, data, state, epochs=3, batchsize=64, verbose=False, rng=np.random.default_rng(1),
+               graphs=graphs)
+        out.append((trainables(chain), list(flow.train_loss), list(flow.valid_loss)))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1] and out[0][2] == out[1][2]

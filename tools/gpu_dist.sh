@@ -12,3 +12,6 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
 unset DF_DIST_BACKEND && \
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
     --master-port 29513 bench.py --gpus 1 --steps 10 --warmup 2 --no-cpu > gpurun_out/dist_1.log 2>&1
+export DF_DIST_BACKEND=gloo && \
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29514 bench.py --gpus 2 --steps 5 --warmup 2 --mode train > gpurun_out/dist_train.log 2>&1
