@@ -28,7 +28,10 @@ enum : int { LIN_BUF = 0, LIN_GATHER = 1 };
 enum : int { LEPI_ACT = 0, LEPI_COUPLE = 1, LEPI_DACT = 2, LEPI_XBAR = 3, LEPI_DACT_XBAR = 4 };
 
 constexpr int kLChunkBytes = 32 * 1024;  // weight chunk (LDS, double-buffered)
-constexpr int kLTiles = 2;               // 16-sample tiles per wave per round
+#ifndef DF_LTILES
+#define DF_LTILES 2
+#endif
+constexpr int kLTiles = DF_LTILES;       // 16-sample tiles per wave per round
 constexpr int kLdwSamples = 32;          // samples per dW staging step
 constexpr int kLdwBM = 8;                // per-wave output blocks (16×16): up to 8 row tiles
 constexpr int kLdwBN = 4;                //   × 4 column tiles (128 accumulator registers)
