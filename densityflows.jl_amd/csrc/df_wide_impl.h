@@ -215,24 +215,31 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
                         *reinterpret_cast<f32x4*>(hs + gs[t] * a.hsave_w + 16 * m + 4 * g) = h[t][m];
         }
         const uint8_t* buf = sg.buf() + lane * 16;
+        // 8 groups (k-quad kk, m-tiles m0..m0+3) per stage; group q+1's fragments are
+        // read while group q's 32 MFMAs run (one wave per SIMD: nothing else would
+        // hide the LDS latency)
+        f32x4 wc[4], wn[4];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const int kq = 2 * st + kk;
+        for (int mm = 0; mm < 4; ++mm) wc[mm] = lds4(buf + mm * 1024);
 #pragma unroll
-            for (int m0 = 0; m0 < 16; m0 += 4) {
-                f32x4 w[4];
+        for (int q = 0; q < 8; ++q) {
+            const int kk = q >> 2, m0 = 4 * (q & 3), kq = 2 * st + kk;
+            if (q + 1 < 8) {
+                const int kk1 = (q + 1) >> 2, m1 = 4 * ((q + 1) & 3);
 #pragma unroll
-                for (int mm = 0; mm < 4; ++mm) w[mm] = lds4(buf + (kk * 16 + m0 + mm) * 1024);
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int mm = 0; mm < 4; ++mm)
-#pragma unroll
-                        for (int t = 0; t < T; ++t)
-                            acc[t][m0 + mm] = mfma4(w[mm][r], h[t][kq][r],
-                                                    (st == 0 && kk == 0 && r == 0) ? f32x4{0.f, 0.f, 0.f, 0.f}
-                                                                                   : acc[t][m0 + mm]);
+                for (int mm = 0; mm < 4; ++mm) wn[mm] = lds4(buf + (kk1 * 16 + m1 + mm) * 1024);
             }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int mm = 0; mm < 4; ++mm)
+#pragma unroll
+                    for (int t = 0; t < T; ++t)
+                        acc[t][m0 + mm] = mfma4(wc[mm][r], h[t][kq][r],
+                                                (st == 0 && kk == 0 && r == 0) ? f32x4{0.f, 0.f, 0.f, 0.f}
+                                                                               : acc[t][m0 + mm]);
+#pragma unroll
+            for (int mm = 0; mm < 4; ++mm) wc[mm] = wn[mm];
         }
     }
     bias_act(N.b1 >= 0 ? a.wbias + N.b1 : nullptr, N.act1, acc, h);
@@ -264,13 +271,15 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
                 }
         }
     } else {
+        f32x4 w0 = lds4(buf);
 #pragma unroll
         for (int kq = 0; kq < 16; ++kq) {
-            const f32x4 w0 = lds4(buf + kq * 1024);
+            const f32x4 wq = w0;
+            if (kq + 1 < 16) w0 = lds4(buf + (kq + 1) * 1024);  // next k-quad in flight
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int t = 0; t < T; ++t) out[t][0] = mfma4(w0[r], h[t][kq][r], out[t][0]);
+                for (int t = 0; t < T; ++t) out[t][0] = mfma4(wq[r], h[t][kq][r], out[t][0]);
         }
     }
 #pragma unroll
