@@ -206,13 +206,14 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
     for (int st = 0; st < 8; ++st) {
         ensure(N.stage0 + N.nst0 + st, sg, a);
         if (hs && st == 0) {  // training: keep H0.  Stored after the stage switch, so the
-                              // stores drain under this stage's MFMAs, not at its vmcnt(0)
+                              // stores drain under this stage's MFMAs, not at its vmcnt(0);
+                              // streaming (non-temporal) so they do not evict the weights from L2
 #pragma unroll
             for (int t = 0; t < T; ++t)
                 if (gs[t] >= 0)
 #pragma unroll
                     for (int m = 0; m < 16; ++m)
-                        *reinterpret_cast<f32x4*>(hs + gs[t] * a.hsave_w + 16 * m + 4 * g) = h[t][m];
+                        __builtin_nontemporal_store(h[t][m], reinterpret_cast<f32x4*>(hs + gs[t] * a.hsave_w + 16 * m + 4 * g));
         }
         const uint8_t* buf = sg.buf() + lane * 16;
         // 8 groups (k-quad kk, m-tiles m0..m0+3) per stage; group q+1's fragments are
@@ -253,7 +254,7 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
             if (gs[t] >= 0)
 #pragma unroll
                 for (int m = 0; m < 16; ++m)
-                    *reinterpret_cast<f32x4*>(hs1 + gs[t] * a.hsave_w + 16 * m + 4 * g) = h[t][m];
+                    __builtin_nontemporal_store(h[t][m], reinterpret_cast<f32x4*>(hs1 + gs[t] * a.hsave_w + 16 * m + 4 * g));
     }
     const uint8_t* buf = sg.buf() + lane * 16;
 #pragma unroll
