@@ -55,6 +55,13 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
         const int n16 = a.w0t_mt * a.w0t_nkq * 64;
         const f32x4* src = reinterpret_cast<const f32x4*>(a.w0t);
         for (int q = threadIdx.x; q < n16; q += kBlockThreads) reinterpret_cast<f32x4*>(w0t_lds)[q] = src[q];
+        // z̄ column of conditioner feature f (0xff: not an identity dim of z; d <= 64),
+        // 64 bytes after the W0ᵀ fragments, fixed for the launch
+        if (threadIdx.x < 64) {
+            const int f = threadIdx.x;
+            const int slot = f < a.n_in ? a.feat[f] : -1;
+            w0t_lds[n16 * 16 + f] = (slot >= a.n && slot < a.n + a.d) ? (uint8_t)(slot - a.n) : (uint8_t)0xff;
+        }
     }
     dma(0, smem);
     if (nchunks == 1 || EPI == LEPI_DACT_XBAR) {
@@ -130,99 +137,126 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
         }
 
         // ---- epilogue: rows 16m + 4g + q of sample smp[t] ----
+        if constexpr (EPI == LEPI_DACT || EPI == LEPI_DACT_XBAR) {
 #pragma unroll
-        for (int t = 0; t < T; ++t) {
-            // LEPI_DACT_XBAR runs an MFMA in its epilogue: keep EXEC full (MFMA operands
-            // cross lanes), guard only the memory accesses
-            if (EPI != LEPI_DACT_XBAR && !valid[t]) continue;
-            const int64_t s = valid[t] ? smp[t] : 0;
+            for (int t = 0; t < T; ++t) {
+                // the σ' arguments of the whole tile are loaded at once (a padding
+                // sample reads the last row; its δ is zeroed and never stored)
+                const int64_t s = valid[t] ? smp[t] : a.batch - 1;
+                constexpr int HR = MT < 8 ? MT : 8;  // σ' arguments in flight
+                const float* hrow = a.hprev + s * a.ld_h + 4 * g;
+                f32x4 h[HR];
 #pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                const int row0 = 16 * m + 4 * g;
-                f32x4 v = acc[t][m];
-                if constexpr (EPI == LEPI_ACT || EPI == LEPI_COUPLE) {
-                    if (a.bias) v = v + *reinterpret_cast<const f32x4*>(a.bias + row0);  // W*x .+ b
-                    if (a.act != DF_ACT_IDENTITY)
+                for (int m = 0; m < HR; ++m) h[m] = *reinterpret_cast<const f32x4*>(hrow + 16 * m);
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) v[q] = impl::act_fn(a.act, v[q]);
-                }
-                if constexpr (EPI == LEPI_ACT) {
-                    *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = v;
-                } else if constexpr (EPI == LEPI_COUPLE) {
-                    // coupling pullback, rrule(RNVP_backward) src/affine/RNVP.jl:133-139
-                    f32x4 dy = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int row = row0 + q;
-                        if (row < a.n_af) {
-                            const int dim = a.af[row] - a.n;
-                            const float zb = a.zbar[s * a.d + dim];
-                            float dq;
-                            if (a.phase == TR_PHASE_S) {
-                                a.ebuf[s * 32 + row] = expf(-v[q]);
-                                dq = -zb * a.u_out[s * a.d + dim] + a.inv_n;  // s̄ = -z̄_af·z_af - j̄
-                            } else {
-                                const bool rnvp = (a.kind == DF_LAYER_RNVP);
-                                const float e = rnvp ? a.ebuf[s * 32 + row] : 1.f;
-                                dq = -zb * e;                                   // t̄ = -z̄_af·exp(-s)
-                                if (rnvp) a.zbar[s * a.d + dim] = zb * e;       // ū_af = z̄_af·exp(-s)
-                            }
-                            if (a.act != DF_ACT_IDENTITY) dq = dq * trn::act_grad(a.act, v[q]);
-                            dy[q] = dq;
-                        }
-                    }
-                    *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = dy;
-                } else if constexpr (EPI == LEPI_DACT || EPI == LEPI_DACT_XBAR) {
-                    const f32x4 h = valid[t] ? *reinterpret_cast<const f32x4*>(a.hprev + s * a.ld_h + row0)
-                                             : f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int m = 0; m < MT; ++m) {
+                    f32x4 v = acc[t][m];
+                    const f32x4 hm = h[m % HR];
+                    if (m + HR < MT) h[m % HR] = *reinterpret_cast<const f32x4*>(hrow + 16 * (m + HR));
                     if (a.dact == DF_ACT_RELU) {
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) v[q] = (h[q] > 0.f) ? v[q] : 0.f;
+                        for (int q = 0; q < 4; ++q) v[q] = (hm[q] > 0.f) ? v[q] : 0.f;
                     } else if (a.dact != DF_ACT_IDENTITY) {
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) v[q] = v[q] * trn::act_grad(a.dact, h[q]);
+                        for (int q = 0; q < 4; ++q) v[q] = v[q] * trn::act_grad(a.dact, hm[q]);
                     }
                     if (!valid[t]) v = f32x4{0.f, 0.f, 0.f, 0.f};
-                    else *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = v;
+                    else *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + 16 * m + 4 * g) = v;
                     if constexpr (EPI == LEPI_DACT_XBAR) acc[t][m] = v;  // δ0 → B operand of W0ᵀ
-                } else {  // LEPI_XBAR: conditioner-input gradient into z̄ of identity dims
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int f = row0 + q;
-                        if (f < a.n_in) {
-                            const int slot = a.feat[f];
-                            if (slot >= a.n && slot < a.n + a.d) a.zbar[s * a.d + (slot - a.n)] += v[q];
-                        }
-                    }
                 }
-            }
-            if constexpr (EPI == LEPI_DACT_XBAR) {
-                // x̄ = W0ᵀ δ0 (rows = conditioner features, <= 4 tiles) → z̄ of identity dims
-                f32x4 xb[4];
+                if constexpr (EPI == LEPI_DACT_XBAR) {
+                    // x̄ = W0ᵀ δ0 (rows = conditioner features, <= 4 tiles) → z̄ of identity dims
+                    // The z̄ entries it adds to are read ahead of the product (their latency
+                    // overlaps its MFMAs), all loads ahead of all stores: distinct features
+                    // of a sample map to distinct state slots (axis_nn).
+                    const uint8_t* zcol = w0t_lds + a.w0t_mt * a.w0t_nkq * 1024;
+                    uint32_t zoff[4];  // the columns of features 16m + 4g + q, a byte per q
+                    float zv[4][4];
 #pragma unroll
-                for (int m = 0; m < 4; ++m) xb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    for (int m = 0; m < 4; ++m) {
+                        if (m < a.w0t_mt) {
+                            zoff[m] = *reinterpret_cast<const uint32_t*>(zcol + 16 * m + 4 * g);
 #pragma unroll
-                for (int kq = 0; kq < MT; ++kq) {
-                    if (kq < a.w0t_nkq) {
-#pragma unroll
-                        for (int m = 0; m < 4; ++m) {
-                            if (m < a.w0t_mt) {
-                                const f32x4 w = lds4(w0t_lds + (kq * a.w0t_mt + m) * 1024 + lane * 16);
-#pragma unroll
-                                for (int q = 0; q < 4; ++q) xb[m] = mfma4(w[q], acc[t][kq][q], xb[m]);
+                            for (int q = 0; q < 4; ++q) {
+                                const uint32_t c = (zoff[m] >> (8 * q)) & 0xffu;
+                                zv[m][q] = a.zbar[s * a.d + (c != 0xffu ? c : 0u)];
                             }
                         }
                     }
-                }
+                    f32x4 xb[4];
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    if (m < a.w0t_mt) {
+                    for (int m = 0; m < 4; ++m) xb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int kq = 0; kq < MT; ++kq) {
+                        if (kq < a.w0t_nkq) {
+#pragma unroll
+                            for (int m = 0; m < 4; ++m) {
+                                if (m < a.w0t_mt) {
+                                    const f32x4 w = lds4(w0t_lds + (kq * a.w0t_mt + m) * 1024 + lane * 16);
+#pragma unroll
+                                    for (int q = 0; q < 4; ++q) xb[m] = mfma4(w[q], acc[t][kq][q], xb[m]);
+                                }
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (m < a.w0t_mt && valid[t]) {
+                                const uint32_t c = (zoff[m] >> (8 * q)) & 0xffu;
+                                if (c != 0xffu) a.zbar[s * a.d + c] = zv[m][q] + xb[m][q];
+                            }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                if (!valid[t]) continue;
+                const int64_t s = smp[t];
+#pragma unroll
+                for (int m = 0; m < MT; ++m) {
+                    const int row0 = 16 * m + 4 * g;
+                    f32x4 v = acc[t][m];
+                    if constexpr (EPI == LEPI_ACT || EPI == LEPI_COUPLE) {
+                        if (a.bias) v = v + *reinterpret_cast<const f32x4*>(a.bias + row0);  // W*x .+ b
+                        if (a.act != DF_ACT_IDENTITY)
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) v[q] = impl::act_fn(a.act, v[q]);
+                    }
+                    if constexpr (EPI == LEPI_ACT) {
+                        *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = v;
+                    } else if constexpr (EPI == LEPI_COUPLE) {
+                        // coupling pullback, rrule(RNVP_backward) src/affine/RNVP.jl:133-139
+                        f32x4 dy = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
-                            const int f = 16 * m + 4 * g + q;
-                            if (valid[t] && f < a.n_in) {
+                            const int row = row0 + q;
+                            if (row < a.n_af) {
+                                const int dim = a.af[row] - a.n;
+                                const float zb = a.zbar[s * a.d + dim];
+                                float dq;
+                                if (a.phase == TR_PHASE_S) {
+                                    a.ebuf[s * 32 + row] = expf(-v[q]);
+                                    dq = -zb * a.u_out[s * a.d + dim] + a.inv_n;  // s̄ = -z̄_af·z_af - j̄
+                                } else {
+                                    const bool rnvp = (a.kind == DF_LAYER_RNVP);
+                                    const float e = rnvp ? a.ebuf[s * 32 + row] : 1.f;
+                                    dq = -zb * e;                                   // t̄ = -z̄_af·exp(-s)
+                                    if (rnvp) a.zbar[s * a.d + dim] = zb * e;       // ū_af = z̄_af·exp(-s)
+                                }
+                                if (a.act != DF_ACT_IDENTITY) dq = dq * trn::act_grad(a.act, v[q]);
+                                dy[q] = dq;
+                            }
+                        }
+                        *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = dy;
+                    } else {  // LEPI_XBAR: conditioner-input gradient into z̄ of identity dims
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const int f = row0 + q;
+                            if (f < a.n_in) {
                                 const int slot = a.feat[f];
-                                if (slot >= a.n && slot < a.n + a.d) a.zbar[s * a.d + (slot - a.n)] += xb[m][q];
+                                if (slot >= a.n && slot < a.n + a.d) a.zbar[s * a.d + (slot - a.n)] += v[q];
                             }
                         }
                     }

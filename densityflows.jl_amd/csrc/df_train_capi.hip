@@ -537,7 +537,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
                     const LOp& op = N.dn[k].bwd;
                     const int nchunks = (op.nkq + op.chunk_kq - 1) / op.chunk_kq;
                     const size_t lds2 = (size_t)(nchunks > 1 ? 2 : 1) * std::min(op.nkq, op.chunk_kq) * op.mt * 1024 +
-                                        (size_t)c2.w0t_mt * c2.w0t_nkq * 1024;
+                                        (size_t)c2.w0t_mt * c2.w0t_nkq * 1024 + 64;  // + z̄ column table
                     c2.wfrag = lb + op.frag;
                     c2.nkq = op.nkq;
                     c2.chunk_kq = op.chunk_kq;
