@@ -103,6 +103,12 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
         };
         f32x4 xn[T];
         load_x(0, xn);  // prefetched one k-quad ahead
+        // DACT epilogues: tile 0's first σ' arguments are loaded during the last k-quad
+        // (the epilogues of all waves otherwise hit HBM in one burst)
+        constexpr bool kDact = (EPI == LEPI_DACT || EPI == LEPI_DACT_XBAR);
+        constexpr int HR = MT < 8 ? MT : 8;  // σ' arguments in flight
+        const int64_t s0h = valid[0] ? smp[0] : a.batch - 1;
+        f32x4 h0[kDact ? HR : 1];
         for (int c = 0; c < nchunks; ++c, ++i) {
             const uint8_t* buf = smem;
             if (nchunks > 1) {
@@ -118,6 +124,13 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
 #pragma unroll
                 for (int t = 0; t < T; ++t) x[t] = xn[t];
                 if (kq + 1 < a.nkq) load_x(kq + 1, xn);
+                if constexpr (kDact) {
+                    if (kq + 1 == a.nkq) {
+#pragma unroll
+                        for (int m = 0; m < HR; ++m)
+                            h0[m] = *reinterpret_cast<const f32x4*>(a.hprev + s0h * a.ld_h + 4 * g + 16 * m);
+                    }
+                }
                 if constexpr (IN == LIN_GATHER) {
 #pragma unroll
                     for (int t = 0; t < T; ++t)
@@ -143,11 +156,10 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
                 // the σ' arguments of the whole tile are loaded at once (a padding
                 // sample reads the last row; its δ is zeroed and never stored)
                 const int64_t s = valid[t] ? smp[t] : a.batch - 1;
-                constexpr int HR = MT < 8 ? MT : 8;  // σ' arguments in flight
                 const float* hrow = a.hprev + s * a.ld_h + 4 * g;
                 f32x4 h[HR];
 #pragma unroll
-                for (int m = 0; m < HR; ++m) h[m] = *reinterpret_cast<const f32x4*>(hrow + 16 * m);
+                for (int m = 0; m < HR; ++m) h[m] = t == 0 ? h0[m] : *reinterpret_cast<const f32x4*>(hrow + 16 * m);
 #pragma unroll
                 for (int m = 0; m < MT; ++m) {
                     f32x4 v = acc[t][m];
