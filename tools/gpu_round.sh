@@ -13,4 +13,6 @@ timeout -k 10 240 python bench.py --config cfg4 --steps 20 --warmup 10 --cpu-sec
 timeout -k 10 240 python bench.py --config cfg1 --steps 200 --warmup 50 --no-cpu > $O/cfg1.json 2> $O/cfg1.err && \
 timeout -k 10 240 python bench.py --mode nll --steps 100 --warmup 20 > $O/nll.json 2> $O/nll.err && \
 timeout -k 10 240 python bench.py --mode train --steps 20 --warmup 5 > $O/train_cfg2.json 2> $O/train_cfg2.err && \
-timeout -k 10 300 python bench.py --mode train --config cfg4 --steps 5 --warmup 2 > $O/train_cfg5.json 2> $O/train_cfg5.err
+timeout -k 10 300 python bench.py --mode train --config cfg4 --steps 5 --warmup 2 > $O/train_cfg5.json 2> $O/train_cfg5.err && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_t5 -o run -- \
+    python3 bench.py --mode train --config cfg4 --steps 2 --warmup 1 > $O/prof_t5.log 2>&1
