@@ -523,12 +523,18 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
     }
 }
 
+// One thread per 4 consecutive features of a sample (rows is a multiple of 16): one
+// 16-byte store; the index arithmetic is 32-bit (the launcher checks the range).
 __global__ void gather_features_kernel(LDenseArgs a, int rows) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.batch * rows) return;
-    const int64_t s = i / rows;
-    const int f = (int)(i - s * rows);
-    a.xsave[s * a.ld_x + f] = (f < a.n_in) ? gather_feature(a, a.feat[f], s) : 0.f;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t rq = (uint32_t)rows >> 2;
+    if (i >= (uint32_t)a.batch * rq) return;
+    const uint32_t s = i / rq;
+    const int f0 = (int)(i - s * rq) * 4;
+    f32x4 v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = (f0 + q < a.n_in) ? gather_feature(a, a.feat[f0 + q], s) : 0.f;
+    *reinterpret_cast<f32x4*>(a.xsave + (int64_t)s * a.ld_x + f0) = v;
 }
 
 template <int MT>
@@ -603,8 +609,9 @@ hipError_t set_couple_bwd_lds_limit(size_t lds) {
 }
 
 hipError_t launch_gather_features(const LDenseArgs& a, int rows, hipStream_t st) {
-    const int64_t n = a.batch * rows;
+    const int64_t n = a.batch * (rows / 4);
     if (n <= 0) return hipSuccess;
+    if (rows % 4 != 0 || a.ld_x % 4 != 0 || n >= (int64_t(1) << 31)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(gather_features_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, rows);
     return hipGetLastError();
 }
