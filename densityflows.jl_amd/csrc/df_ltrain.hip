@@ -302,15 +302,26 @@ __global__ void __launch_bounds__(kBlockThreads, 1) couple_bwd_kernel(LDenseArgs
     const int64_t ntiles = (a.batch + 15) / 16;
     const bool sph = (a.phase == TR_PHASE_S);
     const bool rnvp = (a.kind == DF_LAYER_RNVP);
-    for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wave; tile < ntiles;
-         tile += (int64_t)gridDim.x * kWavesPerBlock) {
+    // H of the next tile is loaded while this one is processed (rows of a padding
+    // sample read the last sample's; its results are never stored)
+    const int64_t tstride = (int64_t)gridDim.x * kWavesPerBlock;
+    f32x4 hn[HT];
+    auto load_h = [&](int64_t tile) {
+        int64_t sl = tile * 16 + j;
+        sl = sl < a.batch ? sl : a.batch - 1;
+#pragma unroll
+        for (int kq = 0; kq < HT; ++kq)
+            hn[kq] = kq < a.nkq ? *reinterpret_cast<const f32x4*>(a.in + sl * a.ld_in + 16 * kq + 4 * g)
+                                : f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    if ((int64_t)blockIdx.x * kWavesPerBlock + wave < ntiles) load_h((int64_t)blockIdx.x * kWavesPerBlock + wave);
+    for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wave; tile < ntiles; tile += tstride) {
         const int64_t s = tile * 16 + j;
         const bool valid = s < a.batch;
         f32x4 h[HT];
 #pragma unroll
-        for (int kq = 0; kq < HT; ++kq)
-            h[kq] = (valid && kq < a.nkq) ? *reinterpret_cast<const f32x4*>(a.in + s * a.ld_in + 16 * kq + 4 * g)
-                                          : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kq = 0; kq < HT; ++kq) h[kq] = hn[kq];
+        if (tile + tstride < ntiles) load_h(tile + tstride);
         f32x4 y[MTO];
 #pragma unroll
         for (int m = 0; m < MTO; ++m) y[m] = f32x4{0.f, 0.f, 0.f, 0.f};
