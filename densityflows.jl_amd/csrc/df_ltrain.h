@@ -32,7 +32,7 @@ constexpr int kLChunkBytes = 32 * 1024;  // weight chunk (LDS, double-buffered)
 #define DF_LTILES 2
 #endif
 constexpr int kLTiles = DF_LTILES;       // 16-sample tiles per wave per round
-constexpr int kLdwSamples = 32;          // samples per dW staging step
+constexpr size_t kLdwLdsMax = 80 * 1024; // dW staging LDS (32 or 64 samples per step)
 constexpr int kLdwBM = 8;                // per-wave output blocks (16×16): up to 8 row tiles
 constexpr int kLdwBN = 4;                //   × 4 column tiles (128 accumulator registers)
 

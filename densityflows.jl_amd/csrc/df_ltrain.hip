@@ -420,12 +420,16 @@ void* couple_bwd_ptr(int ht, int mto) { return mto == 2 ? couple_bwd_ptr_m<2>(ht
 // prefetched into registers while the current one is multiplied.  The 8 waves
 // form a wm × (8/wm) grid over the output tiles; each owns bm × bn 16×16
 // blocks in registers (k-step q of lane group g uses sample 16u + 4g + q).
+// S: samples per staging step (32 for the hidden×hidden dW; 64 for the narrow ones,
+// at most 2 × 2 blocks per wave, whose stages are otherwise too short to cover the
+// two barriers per step)
+template <int S, int BMX, int BNX>  // BMX × BNX: most 16×16 blocks per wave
 __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lsm[];
     const int MA = 16 * a.mta, NB = 16 * a.ntb;
     const int SA = MA + 4, SB = NB + 4;
     float* TA = lsm;
-    float* TB = lsm + kLdwSamples * SA;
+    float* TB = lsm + S * SA;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, j = lane & 15;
     const int wn = kWavesPerBlock / a.wm;
@@ -436,19 +440,19 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
     const int64_t s_end = (s_begin + per < a.batch) ? s_begin + per : a.batch;
     (void)wn;
 
-    f32x4 acc[kLdwBM][kLdwBN];
-    float db[kLdwBM];
+    f32x4 acc[BMX][BNX];
+    float db[BMX];
 #pragma unroll
-    for (int im = 0; im < kLdwBM; ++im) {
+    for (int im = 0; im < BMX; ++im) {
         db[im] = 0.f;
 #pragma unroll
-        for (int in = 0; in < kLdwBN; ++in) acc[im][in] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int in = 0; in < BNX; ++in) acc[im][in] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
     // staging: thread e of a stage loads one f32x4 (sample e / (rows/4), row quad e % (rows/4))
     const int qa = MA / 4, qb = NB / 4;
-    const int na = kLdwSamples * qa, nb = kLdwSamples * qb;
-    constexpr int kPre = (kLdwSamples * 256 / 4 + kBlockThreads - 1) / kBlockThreads;  // per operand
+    const int na = S * qa, nb = S * qb;
+    constexpr int kPre = (S * 256 / 4 + kBlockThreads - 1) / kBlockThreads;  // per operand
     f32x4 pa[kPre], pb[kPre];
     auto fetch = [&](int64_t s0) {
 #pragma unroll
@@ -481,29 +485,29 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
     };
 
     if (s_begin < s_end) fetch(s_begin);
-    for (int64_t s0 = s_begin; s0 < s_end; s0 += kLdwSamples) {
+    for (int64_t s0 = s_begin; s0 < s_end; s0 += S) {
         __syncthreads();  // previous stage consumed
         stash();
         __syncthreads();
-        if (s0 + kLdwSamples < s_end) fetch(s0 + kLdwSamples);
+        if (s0 + S < s_end) fetch(s0 + S);
 #pragma unroll
-        for (int u = 0; u < kLdwSamples / 16; ++u) {
+        for (int u = 0; u < S / 16; ++u) {
             const float* ta = TA + (16 * u + 4 * g) * SA + 16 * m0 + j;
             const float* tb = TB + (16 * u + 4 * g) * SB + 16 * n0 + j;
-            float fb[kLdwBN][4];
+            float fb[BNX][4];
 #pragma unroll
-            for (int in = 0; in < kLdwBN; ++in)
+            for (int in = 0; in < BNX; ++in)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) fb[in][q] = (in < a.bn) ? tb[q * SB + 16 * in] : 0.f;
 #pragma unroll
-            for (int im = 0; im < kLdwBM; ++im) {
+            for (int im = 0; im < BMX; ++im) {
                 if (im < a.bm) {
                     float fa[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) fa[q] = ta[q * SA + 16 * im];
                     if (wj == 0) db[im] += (fa[0] + fa[1]) + (fa[2] + fa[3]);
 #pragma unroll
-                    for (int in = 0; in < kLdwBN; ++in)
+                    for (int in = 0; in < BNX; ++in)
                         if (in < a.bn)
 #pragma unroll
                             for (int q = 0; q < 4; ++q) acc[im][in] = mfma4(fa[q], fb[in][q], acc[im][in]);
@@ -514,11 +518,11 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
 
     float* dst = a.partial + (int64_t)blockIdx.x * a.p_total;
 #pragma unroll
-    for (int im = 0; im < kLdwBM; ++im) {
+    for (int im = 0; im < BMX; ++im) {
         if (im >= a.bm || m0 + im >= a.mta) continue;
         const int ma = m0 + im;
 #pragma unroll
-        for (int in = 0; in < kLdwBN; ++in) {
+        for (int in = 0; in < BNX; ++in) {
             if (in >= a.bn || n0 + in >= a.ntb) continue;
             const int nbk = n0 + in;
 #pragma unroll
@@ -598,7 +602,10 @@ hipError_t set_ldense_lds_limit(size_t lds) {
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    return hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_kernel<32, kLdwBM, kLdwBN>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldw_lds_bytes());
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_kernel<64, 2, 2>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)ldw_lds_bytes());
 }
 
@@ -627,7 +634,12 @@ hipError_t launch_gather_features(const LDenseArgs& a, int rows, hipStream_t st)
     return hipGetLastError();
 }
 
-size_t ldw_lds_bytes() { return (size_t)kLdwSamples * (256 + 4) * 4 * 2; }
+// LDS of one staging step: S samples of both operands (row stride rows + 4 floats)
+static size_t ldw_stage_bytes(int S, int mta, int ntb) { return (size_t)S * (16 * mta + 4 + 16 * ntb + 4) * 4; }
+static int ldw_samples(const LdwArgs& a) {
+    return (a.bm <= 2 && a.bn <= 2 && ldw_stage_bytes(64, a.mta, a.ntb) <= kLdwLdsMax) ? 64 : 32;
+}
+size_t ldw_lds_bytes() { return kLdwLdsMax; }
 
 bool ldw_shape(int mta, int ntb, int* wm, int* bm, int* bn) {
     int best = 1 << 30;
@@ -649,8 +661,10 @@ bool ldw_shape(int mta, int ntb, int* wm, int* bm, int* bn) {
 
 hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st) {
     void* args[] = {const_cast<LdwArgs*>(&a)};
-    return hipLaunchKernel(reinterpret_cast<void*>(&ldw_kernel), dim3(grid), dim3(kBlockThreads), args,
-                           ldw_lds_bytes(), st);
+    const int S = ldw_samples(a);
+    void* fn = S == 64 ? reinterpret_cast<void*>(&ldw_kernel<64, 2, 2>)
+                       : reinterpret_cast<void*>(&ldw_kernel<32, kLdwBM, kLdwBN>);
+    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, ldw_stage_bytes(S, a.mta, a.ntb), st);
 }
 
 }  // namespace df
