@@ -185,6 +185,14 @@ def main():
     s64 = torch.zeros(2, dtype=torch.float64, device=dev)
 
     trainer = None
+    comm = None
+    rehearsal = dist is not None and dist.get_backend() != "nccl"   # gloo: ranks may share one GPU
+    if args.mode != "forward" and not rehearsal:
+        # the library's own RCCL communicator (df_comm) carries every exchange of the
+        # nll / train steps, at every rank count (world 1 included)
+        from densityflows_amd.parallel import DFComm
+
+        comm = DFComm(gpu, rank, world)
     if args.mode == "forward":
         def step():
             hc.run("forward", zbuf, thbuf, xbuf, ldj, B)
@@ -195,25 +203,35 @@ def main():
 
         hc.run("forward", zbuf, thbuf, xbuf, ldj, B)  # data points x = forward(z)
         trainer = HIPTrainer(hc, Adam(1e-3))
-        gview = trainer.grad() if dist is not None else None
 
         def step():
-            if args.graph and dist is None:
+            if args.graph and world == 1:
                 trainer.step_graph(xbuf, thbuf, B, B, s64[:1])
                 return
-            trainer.gradient(xbuf, thbuf, B, B * world, s64[:1])
-            if dist is not None:
-                dist.all_reduce(gview)
-            trainer.apply()
+            if rehearsal:
+                trainer.gradient(xbuf, thbuf, B, B * world, s64[:1])
+                dist.all_reduce(trainer.grad())
+                trainer.apply()
+                return
+            # gradient (global mean) → RCCL all-reduce of ∇ and Σ logpdf → Adam
+            trainer.step_dist(comm, xbuf, thbuf, B, B * world, s64[:1])
     else:
         flow = dfa.Flow(chain, metadata=dfa.MetaData("", d, n, np.zeros(n, np.float32), np.ones(n, np.float32)))
         fh = flow.hip(device=gpu)
         hc.run("forward", zbuf, thbuf, xbuf, ldj, B)  # data points x = forward(z)
 
+        nll = fh.lib.df_flow_nll
+        import ctypes as C
+        from densityflows_amd.hip import _ptr, _stream
+        nll_args = (fh.handle, comm.handle if comm is not None else None, _ptr(xbuf), _ptr(thbuf), C.c_int64(B), C.c_void_p(s64.data_ptr()),
+                    _stream(dev))
+
         def step():
-            fh.run_logpdf_sum(xbuf, thbuf, s64[:1], B)
-            s64[1] = float(B)
-            if dist is not None:
+            # fused inverse + logpdf + fp64 Σ of this rank's shard, {Σ, N} all-reduced over RCCL (df_flow_nll)
+            rc = nll(*nll_args)
+            if rc != 0:
+                raise RuntimeError(fh.lib.df_last_error().decode())
+            if rehearsal:
                 dist.all_reduce(s64)
 
     for _ in range(args.warmup):
@@ -291,6 +309,11 @@ def main():
             out["cpu_baseline"] = cpu_baseline(chain, d, n, seconds=args.cpu_seconds)
             out["vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
+    if args.mode == "nll" and rank == 0:
+        loss = -float(s64[0].item()) / float(s64[1].item())
+        assert s64[1].item() == B * world and np.isfinite(loss), "df_flow_nll returned an inconsistent {Σ, N}"
+    if comm is not None:
+        comm.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -24,6 +24,11 @@ DF_ERR_UNSUPPORTED = -4
 DF_ERR_NOMEM = -5
 DF_ERR_NONFINITE = -6
 
+# df_dtype
+DF_DTYPE_F32 = 0
+DF_DTYPE_F64 = 1
+DF_COMM_ID_BYTES = 128
+
 # df_layer_kind
 DF_LAYER_RNVP = 0
 DF_LAYER_NICE = 1
@@ -54,6 +59,11 @@ class UnsupportedError(NotImplementedError):
 
 class HIPError(RuntimeError):
     """HIP runtime failure inside the library."""
+
+
+class NonFiniteError(ValueError):
+    """DF_ERR_NONFINITE: train!(...; debug=true) found a NaN/Inf loss
+    (src/Flows.jl:404-409 throws an ArgumentError there)."""
 
 
 class df_dense_desc(C.Structure):
@@ -124,6 +134,16 @@ SIGNATURES = {
     "df_train_step_graph": (C.c_int, [_VP, _VP, _VP, _I64, _I64, _VP, _VP]),
     "df_train_get_params": (C.c_int, [_VP, _FP, _I64]),
     "df_train_set_params": (C.c_int, [_VP, _FP, _I64]),
+    "df_train_set_debug": (C.c_int, [_VP, C.c_int]),
+    "df_chain_set_weights": (C.c_int, [_VP, C.POINTER(df_chain_desc)]),
+    "df_comm_get_unique_id": (C.c_int, [_VP]),
+    "df_comm_init_rank": (C.c_int, [C.POINTER(_VP), C.c_int, _VP, C.c_int, C.c_int]),
+    "df_comm_destroy": (C.c_int, [_VP]),
+    "df_comm_get_info": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "df_comm_allreduce_sum": (C.c_int, [_VP, _VP, _I64, C.c_int, _VP]),
+    "df_flow_nll": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _VP]),
+    "df_train_allreduce_gradient": (C.c_int, [_VP, _VP, _VP]),
+    "df_train_step_dist": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _I64, _VP, _VP]),
     "df_device_alloc": (C.c_int, [C.POINTER(_VP), C.c_size_t]),
     "df_device_free": (C.c_int, [_VP]),
     "df_memcpy_h2d": (C.c_int, [_VP, _VP, C.c_size_t, _VP]),
@@ -176,4 +196,6 @@ def check(rc: int, what: str = ""):
         raise UnsupportedError(msg)
     if rc == DF_ERR_NOMEM:
         raise MemoryError(msg)
+    if rc == DF_ERR_NONFINITE:
+        raise NonFiniteError(msg)
     raise HIPError(f"[{rc}] {msg}")

@@ -76,6 +76,18 @@ static int choose_tiles(const df_chain* c, int mode, int64_t batch) {
     return best;
 }
 
+template <typename T>
+static bool same_bytes(const std::vector<T>& a, const std::vector<T>& b) {
+    return a.size() == b.size() && (a.empty() || std::memcmp(a.data(), b.data(), a.size() * sizeof(T)) == 0);
+}
+
+template <typename T>
+static int refresh(const std::vector<T>& v, void* dst) {
+    if (v.empty()) return DF_OK;
+    hipError_t e = hipMemcpy(dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+    return e == hipSuccess ? DF_OK : hip_err(e, "hipMemcpy(weights)");
+}
+
 extern "C" {
 
 int df_get_abi_version(void) { return DF_ABI_VERSION; }
@@ -218,6 +230,53 @@ int df_chain_validate(const df_chain_desc* desc, df_chain_info* info) {
     int rc = df::build_plan(desc, &P, &err);
     if (rc != DF_OK) return set_err(rc, err);
     if (info) fill_info(P, info);
+    return DF_OK;
+}
+
+int df_chain_set_weights(df_chain* c, const df_chain_desc* desc) {
+    if (!c || !desc) return set_err(DF_ERR_INVALID, "null pointer");
+    if (c->n_trainers > 0)
+        return set_err(DF_ERR_INVALID, "df_chain_set_weights: a df_train handle owns the parameters "
+                                       "(use df_train_set_params)");
+    df::Plan P;
+    std::string err;
+    int rc = df::build_plan(desc, &P, &err);
+    if (rc != DF_OK) return set_err(rc, err);
+    const df::Plan& Q = c->plan;
+    // structure: everything but the parameter values (and the ldj constants of the
+    // NormalizationLayers, which follow from x_min / x_max) must be identical
+    const bool same = P.d == Q.d && P.n == Q.n && P.n_layers == Q.n_layers && P.ht == Q.ht && P.tiles == Q.tiles &&
+                      P.outv == Q.outv && P.uniform == Q.uniform && P.relu_only == Q.relu_only && P.fast == Q.fast &&
+                      P.wide == Q.wide && P.stride == Q.stride && P.layers.size() == Q.layers.size() &&
+                      same_bytes(P.denses, Q.denses) && same_bytes(P.chunks, Q.chunks) &&
+                      same_bytes(P.stages, Q.stages) && same_bytes(P.tables, Q.tables) &&
+                      same_bytes(P.sched_fwd, Q.sched_fwd) && same_bytes(P.sched_bwd, Q.sched_bwd) &&
+                      P.blob.size() == Q.blob.size() && P.params.size() == Q.params.size() &&
+                      P.ulayers.size() == Q.ulayers.size() && P.wlayers.size() == Q.wlayers.size() &&
+                      same_bytes(P.wstages, Q.wstages) && P.wblob.size() == Q.wblob.size() &&
+                      P.wbias.size() == Q.wbias.size() && same_bytes(P.pack_dst, Q.pack_dst);
+    if (!same) return set_err(DF_ERR_SHAPE, "df_chain_set_weights: the descriptor's structure differs from the chain's");
+    for (size_t i = 0; i < P.layers.size(); ++i)
+        if (P.layers[i].kind != Q.layers[i].kind || P.layers[i].n_af != Q.layers[i].n_af)
+            return set_err(DF_ERR_SHAPE, "df_chain_set_weights: layer structure differs");
+    DeviceGuard gd(c->device);
+    if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
+    hipError_t e = hipDeviceSynchronize();  // no launch may still read the old weights
+    if (e != hipSuccess) return hip_err(e, "hipDeviceSynchronize");
+    if ((rc = refresh(P.layers, c->d_layers)) != DF_OK || (rc = refresh(P.blob, c->d_blob)) != DF_OK ||
+        (rc = refresh(P.params, c->d_params)) != DF_OK || (rc = refresh(P.ulayers, c->d_ulayers)) != DF_OK)
+        return rc;
+    if (P.wide && ((rc = refresh(P.wlayers, c->d_wlayers)) != DF_OK || (rc = refresh(P.wblob, c->d_wblob)) != DF_OK ||
+                   (rc = refresh(P.wbias, c->d_wbias)) != DF_OK))
+        return rc;
+    c->plan.layers = P.layers;
+    c->plan.ulayers = P.ulayers;
+    c->plan.wlayers = P.wlayers;
+    c->plan.blob.swap(P.blob);
+    c->plan.params.swap(P.params);
+    c->plan.wblob.swap(P.wblob);
+    c->plan.wbias.swap(P.wbias);
+    c->plan.trainables.swap(P.trainables);
     return DF_OK;
 }
 

@@ -52,15 +52,31 @@ __device__ __forceinline__ float relu(float x) {
     return __int_as_float(__builtin_elementwise_max(__float_as_int(x), 0));
 }
 
+// Flux 0.16's Dense evaluates σ = NNlib.fast_act(σ, x): tanh → tanh_fast,
+// sigmoid → sigmoid_fast (Float32 methods, NNlib src/activations.jl).
+// tanh_fast: x·n(x²)/d(x²), evalpoly's muladd Horner chains (fused), sign(x)
+// once x² >= 66 (NaN stays NaN, as Julia's sign).
+__device__ __forceinline__ float tanh_fast(float x) {
+    const float x2 = x * x;
+    const float n = fmaf(fmaf(fmaf(fmaf(1.587199e-8f, x2, 2.2332108e-5f), x2, 0.0035974074f), x2, 0.1346604f), x2, 1.0f);
+    const float d =
+        fmaf(fmaf(fmaf(fmaf(8.7767893e-7f, x2, 0.0003453992f), x2, 0.026262015f), x2, 0.4679937f), x2, 1.0f);
+    return (x2 < 66.f) ? x * (n / d) : (x > 0.f ? 1.f : (x < 0.f ? -1.f : x));
+}
+
+// sigmoid_fast: NNlib.sigmoid with the saturations x > 40 → 1, x < -80 → 0.
+__device__ __forceinline__ float sigmoid_fast(float x) {
+    const float t = expf(-fabsf(x));
+    const float y = (x >= 0.f) ? 1.f / (1.f + t) : t / (1.f + t);
+    return (x > 40.f) ? 1.f : ((x < -80.f) ? 0.f : y);
+}
+
 __device__ __noinline__ float act_fn(int act, float x) {
     switch (act) {
         case DF_ACT_IDENTITY: return x;
         case DF_ACT_RELU: return relu(x);  // max(0, x), NaN-propagating
-        case DF_ACT_TANH: return tanhf(x);
-        case DF_ACT_SIGMOID: {  // NNlib.sigmoid
-            float t = expf(-fabsf(x));
-            return (x >= 0.f) ? 1.f / (1.f + t) : t / (1.f + t);
-        }
+        case DF_ACT_TANH: return tanh_fast(x);
+        case DF_ACT_SIGMOID: return sigmoid_fast(x);
         case DF_ACT_SOFTPLUS: return log1pf(expf(-fabsf(x))) + ((x > 0.f) ? x : 0.f);
         case DF_ACT_LOGCOSH: {  // x + softplus(-2x) - log(2)
             float y = -2.f * x;

@@ -79,6 +79,11 @@ int upload(const std::vector<T>& v, void** dst) {
 
 constexpr double kLog2Pi = 1.8378770664093453;  // log(2π)
 
+// Device ordinal of a df_train handle (df_train_capi.hip; df_comm.hip checks it).
+int train_device(const df_train* t);
+// Device double the last df_train_gradient wrote Σ logpdf to (the caller's or the handle's own).
+double* train_last_lpsum(df_train* t);
+
 // Launch one fused chain pass.  flow: θ normalised with the handle's bounds;
 // snap (inverse modes, specialised kernel): every layer's output kept.
 int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, float* xout, float* ldj, float* lp,

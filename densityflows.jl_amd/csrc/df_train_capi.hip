@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -99,6 +101,9 @@ struct df_train {
     float* d_zbar = nullptr;
     float* d_ebuf = nullptr;
     double* d_lpsum = nullptr;
+    bool debug = false;               // df_train_set_debug: refuse updates on a non-finite loss
+    const double* last_lp = nullptr;  // Σ logpdf written by the last df_train_gradient
+    int64_t last_n = 0;               // ... and the n_total it was taken over
     int64_t cap = 0;       // batch capacity of snap / zbar / ebuf
     int grid = 0;          // workgroups of a full net launch (resident on the device)
     size_t lds_max = 0;
@@ -735,9 +740,11 @@ int df_train_gradient(df_train* t, const float* x, const float* theta_raw, int64
     DeviceGuard gd(c->device);
     if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
     hipStream_t st = static_cast<hipStream_t>(stream);
+    t->last_lp = logpdf_sum ? logpdf_sum : t->d_lpsum;
+    t->last_n = n_total;
     if (batch == 0) {
         hipError_t e = hipMemsetAsync(t->d_grad, 0, sizeof(float) * t->P, st);
-        if (e == hipSuccess && logpdf_sum) e = hipMemsetAsync(logpdf_sum, 0, sizeof(double), st);
+        if (e == hipSuccess) e = hipMemsetAsync(const_cast<double*>(t->last_lp), 0, sizeof(double), st);
         return e == hipSuccess ? DF_OK : hip_err(e, "hipMemsetAsync");
     }
     if (!x) return set_err(DF_ERR_INVALID, "null input array");
@@ -807,6 +814,18 @@ int df_train_apply(df_train* t, void* stream) {
     if (!t) return set_err(DF_ERR_INVALID, "null trainer");
     DeviceGuard gd(t->c->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (t->debug && t->last_lp) {  // train!(...; debug=true), src/Flows.jl:404-409
+        double s = 0.0;
+        hipError_t e = hipMemcpyAsync(&s, t->last_lp, sizeof(double), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return hip_err(e, "debug loss read-back");
+        const double l = -s / (double)(t->last_n > 0 ? t->last_n : 1);
+        if (!std::isfinite(l)) {
+            char msg[96];
+            std::snprintf(msg, sizeof msg, "non-finite training loss %g: parameters not updated", l);
+            return set_err(DF_ERR_NONFINITE, msg);
+        }
+    }
     hipError_t e = launch_adam(t->d_params, t->d_grad, t->d_m, t->d_v, t->P, t->opt.eta, t->opt.beta1,
                                t->opt.beta2, t->opt.epsilon, t->d_bt, st);
     if (e != hipSuccess) return hip_err(e, "Adam kernel launch");
@@ -834,6 +853,10 @@ int df_train_step_graph(df_train* t, const float* x, const float* theta_raw, int
     TrainGraph* g = nullptr;
     for (TrainGraph& e : t->graphs)
         if (e.x == x && e.theta == theta_raw && e.lp == logpdf_sum && e.batch == batch && e.n_total == n_total) g = &e;
+    if (t->debug) {  // the loss check synchronises: no capture while it is on
+        int rc = df_train_gradient(t, x, theta_raw, batch, n_total, logpdf_sum, stream);
+        return rc != DF_OK ? rc : df_train_apply(t, stream);
+    }
     if (g && (g->cap_gen != t->cap_gen || g->partial_gen != t->c->partial_gen)) {  // stale buffers
         if (g->exec) (void)hipGraphExecDestroy(g->exec);
         g->exec = nullptr;
@@ -898,6 +921,12 @@ int df_train_step_graph(df_train* t, const float* x, const float* theta_raw, int
     return e == hipSuccess ? DF_OK : hip_err(e, "hipGraphLaunch(train step)");
 }
 
+int df_train_set_debug(df_train* t, int on) {
+    if (!t) return set_err(DF_ERR_INVALID, "null trainer");
+    t->debug = on != 0;
+    return DF_OK;
+}
+
 int df_train_get_params(df_train* t, float* host_out, int64_t count) {
     if (!t || (!host_out && count > 0)) return set_err(DF_ERR_INVALID, "null pointer");
     if (count != t->P) return set_err(DF_ERR_SHAPE, "count must equal df_train_num_params");
@@ -923,3 +952,10 @@ int df_train_set_params(df_train* t, const float* host_in, int64_t count) {
 }
 
 }  // extern "C"
+
+namespace df {
+namespace api {
+int train_device(const df_train* t) { return t ? t->c->device : -1; }
+double* train_last_lpsum(df_train* t) { return t ? const_cast<double*>(t->last_lp) : nullptr; }
+}  // namespace api
+}  // namespace df

@@ -214,6 +214,15 @@ class HIPChain:
                 pass
             self.handle = None
 
+    def set_weights(self, elements) -> None:
+        """df_chain_set_weights: take the parameters of ``elements`` (same structure)."""
+        flat = flatten_elements(elements)
+        d, n = chain_dims(flat, self.n)
+        if (d, n) != (self.d, self.n):
+            raise _lib.DimensionMismatch("set_weights: (d, n) differ from the chain's")
+        desc = _Desc(flat, d, n)
+        _lib.check(self.lib.df_chain_set_weights(self.handle, C.byref(desc.desc)), "df_chain_set_weights")
+
     def set_theta_bounds(self, tmin, tmax):
         tmin = np.ascontiguousarray(tmin, dtype=np.float32).reshape(-1)
         tmax = np.ascontiguousarray(tmax, dtype=np.float32).reshape(-1)

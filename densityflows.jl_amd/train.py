@@ -105,6 +105,23 @@ class HIPTrainer:
                                                 C.c_int64(n_total), _ptr(lpsum), _stream(self.device)),
                    "df_train_step_graph")
 
+    def set_debug(self, on: bool = True) -> None:
+        """train!(...; debug=true): refuse the Adam update of a non-finite loss
+        (df_train_set_debug → NonFiniteError)."""
+        _lib.check(self.lib.df_train_set_debug(self.handle, 1 if on else 0))
+
+    def allreduce_gradient(self, comm) -> None:
+        """Sum the flat gradient over the ranks of ``comm`` (df_train_allreduce_gradient)."""
+        _lib.check(self.lib.df_train_allreduce_gradient(self.handle, comm.handle, _stream(self.device)),
+                   "df_train_allreduce_gradient")
+
+    def step_dist(self, comm, xbuf, thbuf, batch: int, n_total: int, lpsum=None):
+        """One data-parallel step on this rank's shard (df_train_step_dist):
+        gradient (mean over the global ``n_total``) → RCCL all-reduce → Adam."""
+        _lib.check(self.lib.df_train_step_dist(self.handle, comm.handle if comm is not None else None, _ptr(xbuf),
+                                               _ptr(thbuf), C.c_int64(batch), C.c_int64(n_total), _ptr(lpsum),
+                                               _stream(self.device)), "df_train_step_dist")
+
     def get_params(self) -> np.ndarray:
         out = np.empty(self.num_params, dtype=np.float32)
         _lib.check(self.lib.df_train_get_params(self.handle, out.ctypes.data_as(C.POINTER(C.c_float)),
@@ -177,14 +194,20 @@ def _dist():
     return dist if dist.is_available() and dist.is_initialized() else None
 
 
-def _loss(flow, x, th, group=None):
-    """loss(backward(model, x, θ)...) over a whole set (fused NLL, fp64 sum)."""
+def _loss(flow, x, th, group=None, comm=None):
+    """loss(backward(model, x, θ)...) over a whole set (fused NLL, fp64 sum).
+    With a ``DFComm`` the set is sharded over its ranks and reduced inside the
+    library (df_flow_nll); under a bare torch.distributed group (the gloo
+    rehearsal) the 16-byte partial goes through torch."""
     import torch
 
-    from .parallel import allreduce_nll, shard_range
+    from .parallel import allreduce_nll, flow_nll, shard_range
 
     B = x.shape[1]
     dist = _dist()
+    if comm is not None:
+        a, b = shard_range(B, comm.rank, comm.world)
+        return flow_nll(flow, x[:, a:b], th[:, a:b] if th is not None else None, comm)[0]
     if dist is not None:
         r, w = dist.get_rank(group), dist.get_world_size(group)
         a, b = shard_range(B, r, w)
@@ -197,27 +220,44 @@ def _loss(flow, x, th, group=None):
     return loss
 
 
+def _nonfinite(v: float) -> bool:
+    return not np.isfinite(v)
+
+
 def train_(flow, data, state: TrainState, epochs: int = 100, batchsize: int = 64, shuffle: bool = True,
-           verbose: bool = True, rng=None, group=None, graphs: bool = True):
-    """``train!(flow, data, opt_state; epochs, batchsize, shuffle, verbose)`` — src/Flows.jl:380-445.
+           verbose: bool = True, debug: bool = False, rng=None, group=None, graphs: bool = True, comm=None):
+    """``train!(flow, data, opt_state; epochs, batchsize, shuffle, verbose, debug)`` — src/Flows.jl:380-445.
 
     Per epoch: mini-batches of the training split (Flux.DataLoader: reshuffled
     every epoch when ``shuffle``, last partial batch kept), one gradient + Adam
     step each; then the train and validation losses are pushed to
     ``flow.train_loss`` / ``flow.valid_loss``.  θ is normalised with the
     Flow's MetaData inside the kernels (= normalized_training_data, Data.jl:189).
-    Under torch.distributed every batch is sharded over the ranks and the
-    gradient all-reduced (every rank must pass the same ``rng`` seed).
-    On one device each mini-batch is gathered into a persistent staging buffer
-    and the step (reverse sweep, reduction, Adam, repack) is replayed as one
-    hipGraph (``graphs``; df_train_step_graph), which removes the per-launch
-    host overhead that dominates the reference's default batchsize of 64."""
+
+    ``debug`` (src/Flows.jl:404-409,423-435): a mini-batch whose loss is NaN
+    or ±Inf raises ``ArgumentError`` before its update (the library refuses
+    the Adam step, DF_ERR_NONFINITE); a non-finite epoch train / valid loss
+    prints the reference's message and returns ``backward(model, set...)``
+    = (z, ldj); a run that completes returns (None, None).
+
+    Data parallelism: with ``comm`` (a :class:`DFComm`, one rank per GPU)
+    every batch is sharded over its ranks and each step is
+    ``df_train_step_dist`` (gradient over the global mean → RCCL all-reduce
+    inside the library → Adam); the epoch losses use ``df_flow_nll``.  Under
+    a torch.distributed group without ``comm`` (the CPU/gloo rehearsal) the
+    gradient goes through torch's all-reduce.  Every rank must pass the same
+    ``rng`` seed.  On one device each mini-batch is gathered into a
+    persistent staging buffer and the step (reverse sweep, reduction, Adam,
+    repack) is replayed as one hipGraph (``graphs``; df_train_step_graph),
+    which removes the per-launch host overhead that dominates the reference's
+    default batchsize of 64."""
     import torch
 
     from .parallel import shard_range
 
     rng = rng if rng is not None else np.random.default_rng()
     tr = state.trainer
+    tr.set_debug(debug)
     dev = tr.device
     x_tr, th_tr = data.training_data()
     x_va, th_va = data.validation_data()
@@ -228,7 +268,11 @@ def train_(flow, data, state: TrainState, epochs: int = 100, batchsize: int = 64
     Xs = xt.view(N, flow.d)                                      # row j = sample j
     Ts = tt.view(N, n) if tt is not None else None
     dist = _dist()
-    rank, world = (dist.get_rank(group), dist.get_world_size(group)) if dist is not None else (0, 1)
+    if comm is not None:
+        rank, world = comm.rank, comm.world
+    else:
+        rank, world = (dist.get_rank(group), dist.get_world_size(group)) if dist is not None else (0, 1)
+    local = comm is None and dist is None
     staging = {}  # batch size → persistent (x, θ) device buffers (stable pointers for the graphs)
     for _ in range(epochs):
         order = rng.permutation(N) if shuffle else np.arange(N)
@@ -237,29 +281,56 @@ def train_(flow, data, state: TrainState, epochs: int = 100, batchsize: int = 64
             B = idx.shape[0]
             a, b = shard_range(B, rank, world)
             ii = torch.as_tensor(idx[a:b], device=dev)
-            if dist is None and graphs:
-                if B not in staging:
-                    staging[B] = (torch.empty((B, flow.d), dtype=Xs.dtype, device=dev),
-                                  torch.empty((B, n), dtype=Ts.dtype, device=dev) if Ts is not None else None)
-                xb, tb = staging[B]
-                torch.index_select(Xs, 0, ii, out=xb)
-                if Ts is not None:
-                    torch.index_select(Ts, 0, ii, out=tb)
-                tr.step_graph(xb, tb, B)
-                continue
-            xb = Xs.index_select(0, ii).contiguous()
-            tb = Ts.index_select(0, ii).contiguous() if Ts is not None else None
-            if dist is None:
-                tr.step(xb, tb, B)
-            else:
-                tr.gradient(xb, tb, b - a, B)
-                dist.all_reduce(tr.grad(), op=dist.ReduceOp.SUM, group=group)
-                tr.apply()
-        train_loss = _loss(flow, x_tr, th_tr if n > 0 else None, group)
+            try:
+                if local and graphs:
+                    if B not in staging:
+                        staging[B] = (torch.empty((B, flow.d), dtype=Xs.dtype, device=dev),
+                                      torch.empty((B, n), dtype=Ts.dtype, device=dev) if Ts is not None else None)
+                    xb, tb = staging[B]
+                    torch.index_select(Xs, 0, ii, out=xb)
+                    if Ts is not None:
+                        torch.index_select(Ts, 0, ii, out=tb)
+                    tr.step_graph(xb, tb, B)
+                    continue
+                xb = Xs.index_select(0, ii).contiguous()
+                tb = Ts.index_select(0, ii).contiguous() if Ts is not None else None
+                if local:
+                    tr.step(xb, tb, B)
+                elif comm is not None:
+                    tr.step_dist(comm, xb, tb, b - a, B)
+                else:
+                    tr.gradient(xb, tb, b - a, B)
+                    dist.all_reduce(tr.grad(), op=dist.ReduceOp.SUM, group=group)
+                    if debug:  # the rehearsal's loss check: global Σ logpdf through torch
+                        lp = torch.zeros(1, dtype=torch.float64, device=dev)
+                        if b > a:
+                            flow.hip().logpdf_sum(xb.T, tb.T if tb is not None else None, out=lp)
+                        dist.all_reduce(lp, op=dist.ReduceOp.SUM, group=group)
+                        if _nonfinite(float(lp.item())):
+                            raise _lib.NonFiniteError(f"non-finite training loss {-float(lp.item()) / B}")
+                    tr.apply()
+            except _lib.NonFiniteError as e:
+                raise _lib.ArgumentError(str(e)) from e
+        train_loss = _loss(flow, x_tr, th_tr if n > 0 else None, group, comm)
         flow.train_loss.append(train_loss)
-        valid_loss = _loss(flow, x_va, th_va if n > 0 else None, group)
+        if debug and _nonfinite(train_loss):
+            if rank == 0:
+                print(f"Problem with train loss {train_loss}")
+            state.sync_model()
+            return _backward_set(flow, x_tr, th_tr)
+        valid_loss = _loss(flow, x_va, th_va if n > 0 else None, group, comm)
         flow.valid_loss.append(valid_loss)
+        if debug and _nonfinite(valid_loss):
+            if rank == 0:
+                print(f"Problem with valid loss {valid_loss}")
+            state.sync_model()
+            return _backward_set(flow, x_va, th_va)
         if verbose and rank == 0:
             print(f"epoch: {len(flow.train_loss)} | train_loss = {train_loss}, valid_loss = {valid_loss}")
     state.sync_model()
-    return None
+    return (None, None) if debug else None
+
+
+def _backward_set(flow, x, th):
+    """``backward(flow.model, set...)`` on a normalised data set: (z, ldj)."""
+    return flow.backward(x, th if flow.n > 0 else None)

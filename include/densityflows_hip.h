@@ -148,6 +148,14 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device);
 int df_chain_destroy(df_chain* chain);
 int df_chain_get_info(const df_chain* chain, df_chain_info* out);
 
+/* Replace the chain's parameters (Dense weights and biases, NormalizationLayer
+ * bounds) with those of `desc`, which must describe the same structure (same
+ * layers, axes, widths, activations and bias flags) — e.g. the model after
+ * Optimisers.update! on the host, or one read by load_flow
+ * (src/Loading.jl:324-376).  Synchronous.  Not allowed while df_train handles
+ * are bound to the chain (they own the parameters: df_train_set_params). */
+int df_chain_set_weights(df_chain* chain, const df_chain_desc* desc);
+
 /* θ bounds of the Flow's MetaData (src/Data.jl:75-86; n floats each, host
  * memory).  Enables the df_flow_* entry points' in-kernel θ normalisation. */
 int df_chain_set_theta_bounds(df_chain* chain, const float* theta_min, const float* theta_max);
@@ -197,9 +205,12 @@ int df_flow_logpdf_sum(df_chain* chain, const float* x, const float* theta_raw,
  * Adam state and the gradient buffer, and rewrites the chain's packed
  * weights after every update, so df_chain_* / df_flow_* calls on the chain
  * see the trained parameters.  Supported: chains whose conditioners all have
- * the default _dflt_net shape (src/Layers.jl:33-50) with n_sublayers 1 or 2,
- * hidden width <= 64, <= 4 transformed dims per layer and σ in {identity,
- * relu, tanh, sigmoid}; other chains return DF_ERR_UNSUPPORTED. */
+ * coupling layers whose conditioners have >= 2 Denses of width <= 256 (the
+ * default _dflt_net shape, src/Layers.jl:33-50, with any n_sublayers, e.g. the
+ * hidden-256 config-5 model) and σ in {identity, relu, tanh, sigmoid}.
+ * Conditioners of the hidden <= 64, <= 4-output default shape run one fused
+ * kernel per net; the rest run the layer-wise MFMA path.  Other chains return
+ * DF_ERR_UNSUPPORTED. */
 
 typedef struct df_train df_train;
 
@@ -243,9 +254,59 @@ int df_train_step(df_train* t, const float* x, const float* theta_raw, int64_t b
  * data parallelism (the gradient all-reduce sits between the two halves). */
 int df_train_step_graph(df_train* t, const float* x, const float* theta_raw, int64_t batch, int64_t n_total,
                         double* logpdf_sum, void* stream);
+/* train!(...; debug=true) (src/Flows.jl:404-409): when on, df_train_apply
+ * (and the steps built on it) first reads the Σ logpdf of the last gradient
+ * evaluation back to the host; if the loss is NaN or ±Inf the parameters are
+ * NOT updated and DF_ERR_NONFINITE is returned (the reference throws an
+ * ArgumentError before Optimisers.update!).  Costs one 8-byte device→host
+ * copy and a stream synchronisation per step; df_train_step_graph runs its
+ * steps eagerly while it is on. */
+int df_train_set_debug(df_train* t, int on);
 /* Copy the current trainables to / from host memory (count floats). */
 int df_train_get_params(df_train* t, float* host_out, int64_t count);
 int df_train_set_params(df_train* t, const float* host_in, int64_t count);
+
+/* ---- multi-GPU: one process per GPU, RCCL over xGMI ------------------------
+ * The batch is sharded into contiguous sample blocks (samples are independent
+ * through the chain, src/Chains.jl:149-197); the only exchanges are the sums
+ * the reference's reductions imply:
+ *   loss = -mean(logpdf)  (src/Flows.jl:352-359) → all-reduce {Σ logpdf, count}
+ *   Flux.gradient          (src/Flows.jl:398-411) → all-reduce of the flat ∇
+ * RCCL is resolved at run time (an already-loaded librccl is reused, else
+ * librccl.so.1); without it these calls return DF_ERR_UNSUPPORTED.
+ *
+ * Bootstrap: rank 0 calls df_comm_get_unique_id and ships the
+ * DF_COMM_ID_BYTES bytes to every rank out of band (MPI, a file, a TCP
+ * store); then every rank calls df_comm_init_rank (collective). */
+
+typedef struct df_comm df_comm;
+
+#define DF_COMM_ID_BYTES 128
+
+typedef enum df_dtype { DF_DTYPE_F32 = 0, DF_DTYPE_F64 = 1 } df_dtype;
+
+int df_comm_get_unique_id(void* id_out /* DF_COMM_ID_BYTES */);
+int df_comm_init_rank(df_comm** out, int nranks, const void* id, int rank, int device);
+int df_comm_destroy(df_comm* comm);
+int df_comm_get_info(const df_comm* comm, int* rank, int* nranks, int* device);
+/* In-place sum over all ranks of `count` elements of device memory, ordered
+ * on `stream`. */
+int df_comm_allreduce_sum(df_comm* comm, void* buf_dev, int64_t count, int dtype, void* stream);
+/* The NLL of a sharded batch (config 3): this rank's Σ logpdf of its shard
+ * (df_flow_logpdf_sum) and its sample count are written to sum_count[0..1]
+ * (device doubles) and all-reduced, so on return (stream-ordered) every rank
+ * holds the global {Σ, N}; loss = -Σ / N.  comm = NULL: this process only. */
+int df_flow_nll(df_chain* chain, df_comm* comm, const float* x, const float* theta_raw, int64_t batch,
+                double* sum_count, void* stream);
+/* All-reduce (sum) of the flat gradient of df_train_gradient; every rank must
+ * have called df_train_gradient with n_total = the global batch. */
+int df_train_allreduce_gradient(df_train* t, df_comm* comm, void* stream);
+/* One data-parallel train! step on this rank's shard: df_train_gradient (mean
+ * over n_total, the global batch) → all-reduce of ∇ and of Σ logpdf →
+ * df_train_apply (identical Adam step on every rank).  `logpdf_sum` (device
+ * double or NULL) receives the GLOBAL Σ logpdf.  comm = NULL: one process. */
+int df_train_step_dist(df_train* t, df_comm* comm, const float* x, const float* theta_raw, int64_t batch,
+                       int64_t n_total, double* logpdf_sum, void* stream);
 
 /* ---- device memory helpers (for hosts without a GPU array package) ------ */
 int df_device_alloc(void** ptr, size_t bytes);

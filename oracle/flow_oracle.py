@@ -123,6 +123,61 @@ def _softplus(x):
     return (np.log1p(np.exp(-np.abs(x))) + np.maximum(x, 0)).astype(x.dtype, copy=False)
 
 
+# Flux 0.16 ``Dense`` evaluates ``σ = NNlib.fast_act(a.σ, x)`` (Flux
+# src/layers/basic.jl, ``(a::Dense)(x)``): for Float32/Float64 arrays tanh is
+# replaced by ``tanh_fast`` and σ (sigmoid) by ``sigmoid_fast``.  FAST_ACT
+# selects that Flux-faithful evaluation (the default, and what the HIP kernels
+# compute); ``set_fast_act(False)`` restores the plain NNlib functions.
+FAST_ACT = True
+
+# NNlib.tanh_fast(x::Float32) (NNlib src/activations.jl): a rational
+# approximation of tanh(x)/x in x², Horner-evaluated with muladd by evalpoly
+# (fused on FMA hardware), |x| with x² >= 66 saturating to sign(x).
+_TANH_FAST_N = (1.0, 0.1346604, 0.0035974074, 2.2332108e-5, 1.587199e-8)
+_TANH_FAST_D = (1.0, 0.4679937, 0.026262015, 0.0003453992, 8.7767893e-7)
+
+
+def set_fast_act(on: bool) -> None:
+    global FAST_ACT
+    FAST_ACT = bool(on)
+
+
+def _fma(a, b, c):
+    """fma in the dtype of ``a``: float32 via an exact float64 product (a·b of two
+    float32 is exact in float64; the sum is rounded once more, to float32)."""
+    if a.dtype == np.float32:
+        return (a.astype(np.float64) * np.float64(b) + np.float64(np.float32(c))).astype(np.float32)
+    return a * b + c
+
+
+def _evalpoly(x2, coeffs):
+    dt = x2.dtype.type
+    r = np.full_like(x2, dt(coeffs[-1]))
+    for c in coeffs[-2::-1]:
+        r = _fma(r, x2, dt(c)) if x2.dtype == np.float32 else r * x2 + dt(np.float32(c))
+    return r
+
+
+def tanh_fast(x):
+    """NNlib.tanh_fast on Float32 data (coefficients and saturation of the Float32
+    method; in float64 mode the same function is evaluated in float64)."""
+    dt = x.dtype.type
+    x2 = x * x
+    n = _evalpoly(x2, _TANH_FAST_N)
+    d = _evalpoly(x2, _TANH_FAST_D)
+    with np.errstate(invalid="ignore", over="ignore"):
+        y = x * (n / d)
+    return np.where(x2 < dt(66), y, np.sign(x)).astype(x.dtype, copy=False)
+
+
+def sigmoid_fast(x):
+    """NNlib.sigmoid_fast: sigmoid with ``@fastmath exp`` and the saturations
+    x > 40 → 1, x < -80 → 0."""
+    dt = x.dtype.type
+    y = _sigmoid(x)
+    return np.where(x > dt(40), dt(1), np.where(x < dt(-80), dt(0), y)).astype(x.dtype, copy=False)
+
+
 def activation(name, x):
     """Element-wise activation σ of ``Dense(in, out, σ)`` (Flux / NNlib)."""
     dt = x.dtype.type
@@ -131,9 +186,9 @@ def activation(name, x):
     if name == "relu":
         return np.maximum(x, dt(0))
     if name == "tanh":
-        return np.tanh(x)
+        return tanh_fast(x) if FAST_ACT else np.tanh(x)
     if name == "sigmoid":
-        return _sigmoid(x)
+        return sigmoid_fast(x) if FAST_ACT else _sigmoid(x)
     if name == "softplus":
         return _softplus(x)
     if name == "logcosh":

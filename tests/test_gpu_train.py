@@ -450,3 +450,101 @@ def test_train_graphs_match_eager(cuda):
         out.append((trainables(chain), list(flow.train_loss), list(flow.valid_loss)))
     np.testing.assert_array_equal(out[0][0], out[1][0])
     assert out[0][1] == out[1][1] and out[0][2] == out[1][2]
+
+
+# ---------------------------------------------------------------------------
+# train!(...; debug) and the epoch loop (src/Flows.jl:380-445)
+# ---------------------------------------------------------------------------
+
+def test_debug_refuses_nonfinite_update(cuda):
+    """debug = true: a mini-batch with a non-finite loss raises (DF_ERR_NONFINITE)
+    and leaves the parameters and the Adam state untouched; without debug the
+    update goes through (and poisons the parameters, as in the reference)."""
+    import torch
+
+    from densityflows_amd import _lib
+
+    spec, chain, d, n = _setup("readme")
+    x, th = _inputs(d, n, 256, seed=5)
+    x[2, 17] = np.nan
+    tr = HIPTrainer(chain.hip(), Adam())
+    p0 = tr.get_params().copy()
+    tr.set_debug(True)
+    with pytest.raises(_lib.NonFiniteError):
+        tr.step(_dev(x, cuda), _dev(th, cuda), 256)
+    np.testing.assert_array_equal(tr.get_params(), p0)
+    with pytest.raises(_lib.NonFiniteError):        # the graph-replay entry point checks too
+        tr.step_graph(_dev(x, cuda), _dev(th, cuda), 256)
+    np.testing.assert_array_equal(tr.get_params(), p0)
+    xg, _ = _inputs(d, n, 256, seed=6)              # a finite batch still trains
+    tr.step(_dev(xg, cuda), _dev(th, cuda), 256)
+    assert np.all(np.isfinite(tr.get_params())) and not np.array_equal(tr.get_params(), p0)
+    tr.set_debug(False)
+    tr.step(_dev(x, cuda), _dev(th, cuda), 256)
+    torch.cuda.synchronize()
+    assert not np.all(np.isfinite(tr.get_params()))
+
+
+def _datatest_flow(seed=0):
+    import os
+
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    x = np.load(os.path.join(here, "datatest_x.npy"))
+    th = np.load(os.path.join(here, "datatest_theta.npy"))
+    rng = np.random.default_rng(seed)
+    data = dfa.DataArrays(x, th, rng=rng)
+    chain = dfa.FlowChain(
+        dfa.CouplingLayer(data, [1, 2, 3], hidden_dim_s=16, hidden_dim_t=16, rng=rng),
+        dfa.CouplingLayer(data, [3, 4, 5], hidden_dim_s=16, hidden_dim_t=16, σ="tanh", rng=rng),
+        dfa.CouplingLayer(data, [5, 1, 2], hidden_dim_s=16, hidden_dim_t=16, rng=rng),
+        dfa.NormalizationLayer.from_data(x, -1.0, 1.0))
+    return data, chain, dfa.Flow(chain, data)
+
+
+def test_train_debug_kwarg(cuda):
+    """train_(...; debug=True): NaN in a mini-batch → ArgumentError before its
+    update; a clean run returns (nothing, nothing) like the reference."""
+    from densityflows_amd import _lib
+
+    data, chain, flow = _datatest_flow()
+    state = setup(Adam(1e-3), flow)
+    assert train_(flow, data, state, epochs=1, verbose=False, debug=True, shuffle=False) == (None, None)
+    data.x = data.x.copy()
+    data.x[1, data.partition.training[5]] = np.nan      # first mini-batch (shuffle off)
+    p = trainables(chain).copy()
+    with pytest.raises(_lib.ArgumentError):
+        train_(flow, data, state, epochs=1, verbose=False, debug=True, shuffle=False)
+    np.testing.assert_array_equal(state.trainer.get_params(), p)
+
+
+def test_train_epochs_match_oracle_loop(cuda):
+    """Two epochs of train_ (shuffle off, batchsize 64, partial last batch kept)
+    against the oracle's epoch loop (nll_and_grad + Adam per mini-batch, then
+    the full train / valid losses): the pushed loss vectors agree."""
+    data, chain, flow = _datatest_flow(seed=3)
+    spec0 = chain.to_spec()
+    state = setup(Adam(1e-3), flow)
+    train_(flow, data, state, epochs=2, batchsize=64, shuffle=False, verbose=False, graphs=True)
+    md = flow.metadata
+    x_tr, th_tr = data.training_data()
+    x_va, th_va = data.validation_data()
+    thn_tr = O.normalize_input(th_tr, md.theta_min, md.theta_max)
+    thn_va = O.normalize_input(th_va, md.theta_min, md.theta_max)
+    # oracle loop on a fresh copy of the initial parameters
+    _, chain_o, _ = _datatest_flow(seed=3)
+    p = trainables(chain_o).astype(np.float32)
+    st = [np.zeros_like(p), np.zeros_like(p), (np.float32(0.9), np.float32(0.999))]
+    spec = spec0
+    tl, vl = [], []
+    N = x_tr.shape[1]
+    for _ in range(2):
+        for b0 in range(0, N, 64):
+            _, g = O.nll_and_grad(spec, x_tr[:, b0:b0 + 64], thn_tr[:, b0:b0 + 64])
+            O.adam_update(p, _flat_oracle_grads(spec, g).astype(np.float32), st)
+            load_trainables(chain_o, p)
+            spec = chain_o.to_spec()
+        tl.append(-float(np.mean(O.flow_logpdf(spec, x_tr, thn_tr, np.float64))))
+        vl.append(-float(np.mean(O.flow_logpdf(spec, x_va, thn_va, np.float64))))
+    print("train_loss", flow.train_loss, tl, "valid_loss", flow.valid_loss, vl)
+    np.testing.assert_allclose(flow.train_loss, tl, rtol=2e-4)
+    np.testing.assert_allclose(flow.valid_loss, vl, rtol=2e-4)

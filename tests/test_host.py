@@ -153,3 +153,22 @@ def test_no_gpu_means_loud_failure():
     ch = dfa.FlowChain(dfa.CouplingLayer(5, [1, 2], rng=rng))
     with pytest.raises(dfa.HIPError):
         dfa.forward(ch, np.zeros((5, 4), np.float32))
+
+
+def test_comm_entry_points_fail_cleanly_without_a_device():
+    """df_comm_* are exported and argument-checked on a host without a GPU (the
+    RCCL calls themselves need one: tests/test_gpu_comm.py)."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("host-only check")
+    lib = _lib.load()
+    h = C.c_void_p()
+    uid = C.create_string_buffer(_lib.DF_COMM_ID_BYTES)
+    assert lib.df_comm_init_rank(C.byref(h), 1, uid, 0, 0) != _lib.DF_OK and not h.value
+    assert lib.df_comm_init_rank(C.byref(h), 2, uid, 2, 0) == _lib.DF_ERR_INVALID   # rank out of range
+    assert lib.df_comm_destroy(None) == _lib.DF_OK
+    assert lib.df_comm_allreduce_sum(None, None, 4, _lib.DF_DTYPE_F32, None) == _lib.DF_ERR_INVALID
+    assert lib.df_flow_nll(None, None, None, None, 4, None, None) == _lib.DF_ERR_INVALID
+    assert lib.df_train_set_debug(None, 1) == _lib.DF_ERR_INVALID
+    assert lib.df_chain_set_weights(None, None) == _lib.DF_ERR_INVALID
