@@ -55,6 +55,8 @@ struct LDenseArgs {
     // epilogue
     float* out;             // [B][ld_out]
     int ld_out;
+    float* dsave;           // LEPI_ACT: σ'(pre-activation) stored [B][ld_out] (nets with a
+                            // softplus / logcosh / swish σ), or nullptr
     const float* hprev;     // LEPI_DACT: σ'(hprev) with activation dact
     int ld_h, dact;
     float* zbar;            // LEPI_COUPLE / LEPI_XBAR

@@ -230,14 +230,22 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
                 for (int m = 0; m < MT; ++m) {
                     const int row0 = 16 * m + 4 * g;
                     f32x4 v = acc[t][m];
+                    f32x4 pre = v;
                     if constexpr (EPI == LEPI_ACT || EPI == LEPI_COUPLE) {
                         if (a.bias) v = v + *reinterpret_cast<const f32x4*>(a.bias + row0);  // W*x .+ b
+                        pre = v;
                         if (a.act != DF_ACT_IDENTITY)
 #pragma unroll
                             for (int q = 0; q < 4; ++q) v[q] = impl::act_fn(a.act, v[q]);
                     }
                     if constexpr (EPI == LEPI_ACT) {
                         *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = v;
+                        if (a.dsave) {  // σ'(x) for a pre-activation σ (trn::kDactStored)
+                            f32x4 dv;
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) dv[q] = trn::act_dx(a.act, pre[q], v[q]);
+                            *reinterpret_cast<f32x4*>(a.dsave + s * a.ld_out + row0) = dv;
+                        }
                     } else if constexpr (EPI == LEPI_COUPLE) {
                         // coupling pullback, rrule(RNVP_backward) src/affine/RNVP.jl:133-139
                         f32x4 dy = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -257,7 +265,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
                                     dq = -zb * e;                                   // t̄ = -z̄_af·exp(-s)
                                     if (rnvp) a.zbar[s * a.d + dim] = zb * e;       // ū_af = z̄_af·exp(-s)
                                 }
-                                if (a.act != DF_ACT_IDENTITY) dq = dq * trn::act_grad(a.act, v[q]);
+                                if (a.act != DF_ACT_IDENTITY) dq = dq * trn::act_dx(a.act, pre[q], v[q]);
                                 dy[q] = dq;
                             }
                         }
@@ -343,6 +351,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) couple_bwd_kernel(LDenseArgs
             const int row0 = 16 * m + 4 * g;
             f32x4 v = y[m];
             if (a.bias) v = v + *reinterpret_cast<const f32x4*>(a.bias + row0);
+            const f32x4 pre = v;
             if (a.act != DF_ACT_IDENTITY)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = impl::act_fn(a.act, v[q]);
@@ -362,7 +371,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) couple_bwd_kernel(LDenseArgs
                         dq = -zb * e;                                   // t̄ = -z̄_af·exp(-s)
                         if (rnvp) a.zbar[s * a.d + dim] = zb * e;       // ū_af = z̄_af·exp(-s)
                     }
-                    if (a.act != DF_ACT_IDENTITY) dq = dq * trn::act_grad(a.act, v[q]);
+                    if (a.act != DF_ACT_IDENTITY) dq = dq * trn::act_dx(a.act, pre[q], v[q]);
                     dy[m][q] = dq;
                 }
             }

@@ -27,6 +27,16 @@ namespace df {
 
 constexpr int kTS = 20;  // row stride (floats) of the per-wave transpose buffers [row][16 samples]
 
+namespace trn {
+// Activation modes of the training kernels: σ' from the output alone, relu-only,
+// or σ' of softplus / logcosh / swish, which needs the pre-activation.
+enum { AM_Y = 0, AM_RELU = 1, AM_PRE = 2 };
+
+// σ' applied by the layer-wise δ kernels when the factor was stored at recompute
+// time (nets with a pre-activation σ): hprev then holds σ'(x) itself.
+constexpr int kDactStored = 64;
+}  // namespace trn
+
 // One conditioner net of the specialised shape, as the training kernel sees it.
 struct GNet {
     UNet u;                  // forward fragments (offsets rebased to the net's own LDS copy)
@@ -66,9 +76,9 @@ struct TrainArgs {
 
 size_t train_net_lds(int ht, const GNet& g);
 hipError_t set_train_lds_limit(size_t lds);
-hipError_t launch_train_net(int ht, int nh, bool relu, const TrainArgs& a, unsigned grid, size_t lds,
+hipError_t launch_train_net(int ht, int nh, int am, const TrainArgs& a, unsigned grid, size_t lds,
                             hipStream_t st);
-hipError_t train_net_occupancy(int ht, int nh, bool relu, size_t lds, int* blocks);
+hipError_t train_net_occupancy(int ht, int nh, int am, size_t lds, int* blocks);
 
 hipError_t launch_scale(float* dst, const float* src, float s, int64_t count, hipStream_t st);
 hipError_t launch_norm_adjoint(float* zbar, const float* xmin, const float* xmax, float alpha, float beta, int d,

@@ -8,10 +8,14 @@ namespace df {
 
 namespace {
 
-void* train_ptr(int ht, int nh, bool relu) {
-#define DF_T(H)                                                                                   \
-    (nh ? (relu ? train_kernel_ptr<H, 1, true>() : train_kernel_ptr<H, 1, false>())               \
-        : (relu ? train_kernel_ptr<H, 0, true>() : train_kernel_ptr<H, 0, false>()))
+void* train_ptr(int ht, int nh, int am) {
+#define DF_T(H)                                                                                           \
+    (nh ? (am == trn::AM_RELU ? train_kernel_ptr<H, 1, trn::AM_RELU>()                                   \
+                              : (am == trn::AM_PRE ? train_kernel_ptr<H, 1, trn::AM_PRE>()                \
+                                                   : train_kernel_ptr<H, 1, trn::AM_Y>()))                \
+        : (am == trn::AM_RELU ? train_kernel_ptr<H, 0, trn::AM_RELU>()                                   \
+                              : (am == trn::AM_PRE ? train_kernel_ptr<H, 0, trn::AM_PRE>()                \
+                                                   : train_kernel_ptr<H, 0, trn::AM_Y>())))
     switch (ht) {
         case 1: return DF_T(1);
         case 2: return DF_T(2);
@@ -111,24 +115,24 @@ size_t train_net_lds(int ht, const GNet& g) {
 hipError_t set_train_lds_limit(size_t lds) {
     for (int ht : {1, 2, 4})
         for (int nh = 0; nh < 2; ++nh)
-            for (int relu = 0; relu < 2; ++relu) {
-                hipError_t e = hipFuncSetAttribute(train_ptr(ht, nh, relu != 0),
+            for (int am = 0; am < 3; ++am) {
+                hipError_t e = hipFuncSetAttribute(train_ptr(ht, nh, am),
                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 if (e != hipSuccess) return e;
             }
     return hipSuccess;
 }
 
-hipError_t launch_train_net(int ht, int nh, bool relu, const TrainArgs& a, unsigned grid, size_t lds,
+hipError_t launch_train_net(int ht, int nh, int am, const TrainArgs& a, unsigned grid, size_t lds,
                             hipStream_t st) {
-    void* k = train_ptr(ht, nh, relu);
+    void* k = train_ptr(ht, nh, am);
     if (!k) return hipErrorInvalidValue;
     void* args[] = {const_cast<TrainArgs*>(&a)};
     return hipLaunchKernel(k, dim3(grid), dim3(kBlockThreads), args, lds, st);
 }
 
-hipError_t train_net_occupancy(int ht, int nh, bool relu, size_t lds, int* blocks) {
-    void* k = train_ptr(ht, nh, relu);
+hipError_t train_net_occupancy(int ht, int nh, int am, size_t lds, int* blocks) {
+    void* k = train_ptr(ht, nh, am);
     if (!k) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k, kBlockThreads, lds);
 }

@@ -52,11 +52,14 @@ struct LDense {
 
 struct LNet {
     std::vector<LDense> dn;  // Dense(in,h,σ0), hidden..., Dense(h,out,σo)
+    bool pre = false;        // a hidden σ needs its pre-activation for σ' (softplus, logcosh, swish):
+                             // the sweep recomputes the net and stores σ'(x) beside H
 };
 
-bool act_trainable(int a) {
-    return a == DF_ACT_IDENTITY || a == DF_ACT_RELU || a == DF_ACT_TANH || a == DF_ACT_SIGMOID;
-}
+// every activation the plan accepts has a derivative rule (df_train_impl.h act_grad/act_dx)
+bool act_trainable(int a) { return a >= DF_ACT_IDENTITY && a <= DF_ACT_SWISH; }
+
+bool act_needs_pre(int a) { return a == DF_ACT_SOFTPLUS || a == DF_ACT_LOGCOSH || a == DF_ACT_SWISH; }
 
 }  // namespace
 
@@ -81,7 +84,7 @@ struct df_train {
     std::vector<TrainGraph> graphs;
     uint64_t use_clock = 0;
     int64_t P = 0;
-    int relu = 0;
+    int amode = 0;                    // fused kernel activation mode (trn::AM_*)
     std::vector<GNet> nets;
     std::vector<int> net_nh;
     std::vector<SweepOp> ops;
@@ -119,6 +122,8 @@ struct df_train {
     int lwidth = 16;                 // widest activation row (floats)
     int lmax_h = 1;                  // activation buffers needed (hidden Denses + 1)
     std::vector<float*> d_lh, d_ld; // H_k and δ_k buffers [cap][lwidth]
+    std::vector<float*> d_lv;       // σ'(x_k) buffers [cap][lwidth] (nets with LNet::pre)
+    bool any_pre = false;
     float* d_ly = nullptr;           // ȳ  [cap][lwidth]
     float* d_lx = nullptr;           // gathered conditioner input [cap][lwidth]
     // hidden activations kept by the inverse pass (generic kernel): the sweep then
@@ -155,6 +160,8 @@ void free_all(df_train* t) {
     for (float* p : t->d_lh)
         if (p) (void)hipFree(p);
     for (float* p : t->d_ld)
+        if (p) (void)hipFree(p);
+    for (float* p : t->d_lv)
         if (p) (void)hipFree(p);
 }
 
@@ -215,7 +222,7 @@ int build_lnets(df_train* t) {
             for (int k = 0; k < nd; ++k) {
                 const DevDense& DD = P.denses[d0 + k];
                 if (!act_trainable(DD.act))
-                    return set_err(DF_ERR_UNSUPPORTED, "training supports σ ∈ {identity, relu, tanh, sigmoid}");
+                    return set_err(DF_ERR_UNSUPPORTED, "unknown activation");
                 LDense D;
                 D.in_dim = DD.in_dim;
                 D.out_dim = DD.n_out;
@@ -226,10 +233,12 @@ int build_lnets(df_train* t) {
                 pack_lbias(t, P, D, D.fwd);
                 D.bwd = pack_lop(t, P, D, true);
                 t->lwidth = std::max({t->lwidth, 16 * D.fwd.mt, 16 * D.bwd.mt});
+                if (k + 1 < nd && act_needs_pre(D.act)) net.pre = true;
                 net.dn.push_back(D);
             }
             if (nd < 2) return set_err(DF_ERR_UNSUPPORTED, "training needs conditioners of >= 2 Dense layers");
             t->lmax_h = std::max(t->lmax_h, nd - 1);
+            t->any_pre = t->any_pre || net.pre;
             t->lnets.push_back(net);
             t->ops.push_back({li, (int)t->lnets.size() - 1, phase});
             return DF_OK;
@@ -302,7 +311,7 @@ int build_nets(df_train* t) {
             const DevDense& DO = P.denses[d0 + nd - 1];
             for (int k = 0; k < nd; ++k)
                 if (!act_trainable(P.denses[d0 + k].act))
-                    return set_err(DF_ERR_UNSUPPORTED, "training supports σ ∈ {identity, relu, tanh, sigmoid}");
+                    return set_err(DF_ERR_UNSUPPORTED, "unknown activation");
             GNet g{};
             g.u = u0;
             g.n_in = D0.in_dim;
@@ -364,7 +373,7 @@ int ensure_capacity(df_train* t, int64_t batch) {
             (void)hipFree(*p);
             *p = nullptr;
         }
-    for (auto* v : {&t->d_lh, &t->d_ld}) {
+    for (auto* v : {&t->d_lh, &t->d_ld, &t->d_lv}) {
         for (float* p : *v)
             if (p) (void)hipFree(p);
         v->clear();
@@ -399,6 +408,12 @@ int ensure_capacity(df_train* t, int64_t batch) {
             }
             t->d_lh.push_back(h);
             t->d_ld.push_back(dl);
+            if (t->any_pre && k < t->lmax_h) {
+                float* dv = nullptr;
+                if (hipMalloc(reinterpret_cast<void**>(&dv), row) != hipSuccess)
+                    return set_err(DF_ERR_NOMEM, "hipMalloc failed (training activations)");
+                t->d_lv.push_back(dv);
+            }
         }
     }
     t->cap = cap;
@@ -479,17 +494,24 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         b.ld_in = b.ld_out = b.ld_h = b.ld_x = W;
         // H_k: kept by the inverse pass, or recomputed here
         const int net_slot = 2 * op.layer + (op.phase == TR_PHASE_T ? 1 : 0);
+        // a net with a pre-activation σ is recomputed here (σ'(x) is stored beside H)
+        const bool keep = t->hsave_on && !N.pre;
         auto H = [&](int k) -> float* {
-            return t->hsave_on ? t->d_hsave + ((int64_t)net_slot * t->lmax_h + k) * batch * W : t->d_lh[k];
+            return keep ? t->d_hsave + ((int64_t)net_slot * t->lmax_h + k) * batch * W : t->d_lh[k];
+        };
+        // σ' argument of Dense k's output: H_k, or the stored σ'(x_k)
+        auto DACT = [&](int k, LDenseArgs& a) {
+            a.hprev = N.pre ? t->d_lv[k] : H(k);
+            a.dact = N.pre ? trn::kDactStored : N.dn[k].act;
         };
         // fused backward front (needs the kept activations, <= 32 outputs, hidden <= 256)
-        const bool fused = t->hsave_on && N.dn[nd - 1].fwd.mt <= 2 && N.dn[0].bwd.mt <= 4 &&
+        const bool fused = keep && N.dn[nd - 1].fwd.mt <= 2 && N.dn[0].bwd.mt <= 4 &&
                            !(std::getenv("DF_TRAIN_NOFUSE") && std::getenv("DF_TRAIN_NOFUSE")[0] == '1');
         // forward (recompute): H_k = σ(W_k · in + b_k), then the output Dense + coupling pullback → ȳ
         for (int k = 0; k < nd - (fused ? 1 : 0); ++k) {
             LDenseArgs a = b;
             a.act = N.dn[k].act;
-            if (k + 1 < nd && t->hsave_on) {
+            if (k + 1 < nd && keep) {
                 if (k == 0) {
                     a.xsave = t->d_lx;
                     e = e == hipSuccess ? launch_gather_features(a, 16 * N.dn[0].bwd.mt, st) : e;
@@ -503,6 +525,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             }
             if (k + 1 < nd) {
                 a.out = H(k);
+                a.dsave = N.pre ? t->d_lv[k] : nullptr;
                 dense(N.dn[k].fwd, k == 0 ? LIN_GATHER : LIN_BUF, LEPI_ACT, a);
             } else {
                 a.out = t->d_ly;
@@ -532,8 +555,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             for (int k = nd - 2; k >= 1; --k) {
                 LDenseArgs c2 = b;
                 c2.in = gcur;
-                c2.hprev = H(k - 1);
-                c2.dact = N.dn[k - 1].act;
+                DACT(k - 1, c2);
                 c2.out = t->d_ld[k - 1];
                 if (k == 1) {
                     c2.w0t = lb + N.dn[0].bwd.frag;
@@ -561,8 +583,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         for (int k = nd - 1; k >= 1 && !fused; --k) {
             LDenseArgs a = b;
             a.in = gcur;
-            a.hprev = H(k - 1);
-            a.dact = N.dn[k - 1].act;
+            DACT(k - 1, a);
             a.out = t->d_ld[k - 1];
             dense(N.dn[k].bwd, LIN_BUF, LEPI_DACT, a);
             gcur = t->d_ld[k - 1];
@@ -625,7 +646,9 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
     }
     const Plan& P = c->plan;
     t->P = (int64_t)P.trainables.size();
-    t->relu = P.relu_only;
+    t->amode = P.relu_only ? trn::AM_RELU : trn::AM_Y;
+    for (const DevDense& D : P.denses)
+        if (act_needs_pre(D.act) && !P.relu_only) t->amode = trn::AM_PRE;
     // fused per-net kernel when every conditioner fits its registers, else layer-wise
     const char* force = std::getenv("DF_TRAIN_LAYERWISE");
     int rc = (force && force[0] == '1') ? DF_ERR_UNSUPPORTED : build_nets(t);
@@ -663,7 +686,7 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
     int occ = 1;
     for (size_t i = 0; i < t->nets.size(); ++i) {
         int b = 1;
-        if (train_net_occupancy(P.ht, t->net_nh[i], t->relu != 0, t->lds_max, &b) == hipSuccess && b >= 1)
+        if (train_net_occupancy(P.ht, t->net_nh[i], t->amode, t->lds_max, &b) == hipSuccess && b >= 1)
             occ = (i == 0) ? b : std::min(occ, b);
     }
     t->grid = std::max(1, c->n_cu * occ);
@@ -802,7 +825,7 @@ int df_train_gradient(df_train* t, const float* x, const float* theta_raw, int64
         a.phase = op.phase;
         a.inv_n = inv_n;
         a.net = t->nets[op.net];
-        e = launch_train_net(P.ht, t->net_nh[op.net], t->relu != 0, a, (unsigned)grid, t->lds_max, st);
+        e = launch_train_net(P.ht, t->net_nh[op.net], t->amode, a, (unsigned)grid, t->lds_max, st);
         if (e != hipSuccess) return hip_err(e, "train kernel launch");
     }
     // 4. fixed-order reduction of the workgroup partials

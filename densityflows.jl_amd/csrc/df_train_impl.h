@@ -30,14 +30,47 @@ using impl::mfma4;
 
 __device__ __forceinline__ f32x4 lds4f(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
-// σ'(x) from y = σ(x) (ChainRules / NNlib derivative rules)
+// σ'(x) from y = σ(x): NNlib's derivative table (src/activations.jl, UNARY_ACTS)
+// for the activations whose rule is written in Ω alone.
 __device__ __forceinline__ float act_grad(int act, float y) {
     switch (act) {
         case DF_ACT_RELU: return y > 0.f ? 1.f : 0.f;
-        case DF_ACT_TANH: return 1.f - y * y;
-        case DF_ACT_SIGMOID: return y * (1.f - y);
+        case DF_ACT_TANH: return 1.f - y * y;                     // tanh_fast: 1 - Ω²
+        case DF_ACT_SIGMOID: return y * (1.f - y);                // sigmoid_fast: Ω(1 - Ω)
+        case DF_ACT_LEAKYRELU: return y > 0.f ? 1.f : 0.01f;      // ifelse(Ω > 0, 1, 1//100)
+        case DF_ACT_ELU: return y >= 0.f ? 1.f : y + 1.f;         // deriv_elu(Ω) = ifelse(Ω ≥ 0, 1, Ω + α)
+        case kDactStored: return y;
         default: return 1.f;
     }
+}
+
+__device__ __forceinline__ bool act_needs_pre(int act) {
+    return act == DF_ACT_SOFTPLUS || act == DF_ACT_LOGCOSH || act == DF_ACT_SWISH;
+}
+
+// σ'(x) from the pre-activation x and y = σ(x) (NNlib: softplus → sigmoid_fast(x),
+// logcosh → tanh(x), swish → Ω + sigmoid_fast(x)·(1 − Ω)); the rest as act_grad.
+__device__ __forceinline__ float act_dx(int act, float x, float y) {
+    switch (act) {
+        case DF_ACT_SOFTPLUS: return impl::sigmoid_fast(x);
+        case DF_ACT_LOGCOSH: return tanhf(x);
+        case DF_ACT_SWISH: return y + impl::sigmoid_fast(x) * (1.f - y);
+        default: return act_grad(act, y);
+    }
+}
+
+// v = σ.(v) in place, σ'(pre) into dv (AM_PRE recompute)
+template <int HT>
+__device__ __forceinline__ void act_keep_grad(int act, f32x4 (&v)[HT], f32x4 (&dv)[HT]) {
+#pragma unroll
+    for (int m = 0; m < HT; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float x = v[m][r];
+            const float y = (act == DF_ACT_IDENTITY) ? x : impl::act_fn(act, x);
+            dv[m][r] = act_dx(act, x, y);
+            v[m][r] = y;
+        }
 }
 
 template <int HT, bool RELU>
@@ -71,9 +104,11 @@ __device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)
 
 }  // namespace trn
 
-template <int HT, int NH, bool RELU>
+template <int HT, int NH, int AM>
 __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a) {
     using namespace trn;
+    constexpr bool RELU = (AM == AM_RELU);
+    constexpr bool PRE = (AM == AM_PRE);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const GNet& G = a.net;
     const UNet& N = G.u;
@@ -146,15 +181,39 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
 
         // ---- forward recompute ----
         f32x4 A0[1][HT], A1[1][HT];
+        constexpr int NP = PRE ? HT : 1;
+        f32x4 D0[NP], D1[NP];  // AM_PRE: σ'(pre) of the first / hidden Dense
         uni::dense_first<HT, 1>(fw, N, xin, A0);
-        uni::bias_act<HT, 1, RELU>(fw + N.off_b0, N.act0, A0, !N.fold0);
+        if constexpr (PRE) {
+            uni::bias_act<HT, 1, false>(fw + N.off_b0, DF_ACT_IDENTITY, A0, !N.fold0);
+            act_keep_grad<HT>(N.act0, A0[0], D0);
+        } else {
+            uni::bias_act<HT, 1, RELU>(fw + N.off_b0, N.act0, A0, !N.fold0);
+        }
         if constexpr (NH == 1) {
             uni::dense_hidden<HT, 1>(fw + N.off_h, A0, A1);
-            uni::bias_act<HT, 1, RELU>(fw + N.off_h + HT * HT * 1024, N.acth, A1);
+            if constexpr (PRE) {
+                uni::bias_act<HT, 1, false>(fw + N.off_h + HT * HT * 1024, DF_ACT_IDENTITY, A1);
+                act_keep_grad<HT>(N.acth, A1[0], D1);
+            } else {
+                uni::bias_act<HT, 1, RELU>(fw + N.off_h + HT * HT * 1024, N.acth, A1);
+            }
         }
         const f32x4(&H)[1][HT] = NH ? A1 : A0;
         f32x4 o[1];
-        uni::out_valu<HT, 1, RELU>(fw, N, H, o);
+        float dfo[4] = {1.f, 1.f, 1.f, 1.f};  // AM_PRE: σo'(pre) of the output Dense
+        if constexpr (PRE) {
+            uni::out_valu<HT, 1, true>(fw, N, H, o);  // pre-activation (no σo)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float x = o[0][k];
+                const float y = (N.act_out == DF_ACT_IDENTITY) ? x : impl::act_fn(N.act_out, x);
+                dfo[k] = act_dx(N.act_out, x, y);
+                o[0][k] = y;
+            }
+        } else {
+            uni::out_valu<HT, 1, RELU>(fw, N, H, o);
+        }
 
         // ---- coupling pullback → ȳ (every lane group holds all outputs of sample j) ----
         float dout[4], zb[4], ee[4];
@@ -173,7 +232,11 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
                     if (rnvp) ee[k] = a.ebuf[s * 4 + k];
                     dout[k] = -zb[k] * ee[k];                              // t̄ = -z̄_af·exp(-s)
                 }
-                if (!RELU && N.act_out != DF_ACT_IDENTITY) dout[k] = dout[k] * act_grad(N.act_out, o[0][k]);
+                if (PRE) {
+                    if (N.act_out != DF_ACT_IDENTITY) dout[k] = dout[k] * dfo[k];
+                } else if (!RELU && N.act_out != DF_ACT_IDENTITY) {
+                    dout[k] = dout[k] * act_grad(N.act_out, o[0][k]);
+                }
             }
         }
         if (sph && g == 0 && valid) {
@@ -212,7 +275,13 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
                 }
             }
         }
-        mul_act_grad<HT, RELU>(NH ? N.acth : N.act0, H[0], hb[0]);
+        if constexpr (PRE) {
+            const f32x4(&DH)[NP] = NH ? D1 : D0;
+#pragma unroll
+            for (int m = 0; m < HT; ++m) hb[0][m] = hb[0][m] * DH[m];
+        } else {
+            mul_act_grad<HT, RELU>(NH ? N.acth : N.act0, H[0], hb[0]);
+        }
 
         // ---- hidden Dense: dW1 += δ·A0ᵀ, db1 += Σδ, Ā0 = W1ᵀ δ ----
         f32x4 d0[1][HT];
@@ -235,7 +304,12 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
 #pragma unroll
                     for (int mb = 0; mb < HT; ++mb) gWh[ma][mb] = mfma4(fa[ma][q], fb[mb][q], gWh[ma][mb]);
             uni::dense_hidden<HT, 1>(tw + G.off_ht, hb, d0);
-            mul_act_grad<HT, RELU>(N.act0, A0[0], d0[0]);
+            if constexpr (PRE) {
+#pragma unroll
+                for (int m = 0; m < HT; ++m) d0[0][m] = d0[0][m] * D0[m];
+            } else {
+                mul_act_grad<HT, RELU>(N.act0, A0[0], d0[0]);
+            }
         } else {
 #pragma unroll
             for (int m = 0; m < HT; ++m) d0[0][m] = hb[0][m];
@@ -336,9 +410,9 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
     for (int i = tid; i < G.p_count; i += kBlockThreads) dst[i] = R[i];
 }
 
-template <int HT, int NH, bool RELU>
+template <int HT, int NH, int AM>
 void* train_kernel_ptr() {
-    return reinterpret_cast<void*>(&train_net_kernel<HT, NH, RELU>);
+    return reinterpret_cast<void*>(&train_net_kernel<HT, NH, AM>);
 }
 
 }  // namespace df

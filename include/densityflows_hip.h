@@ -204,13 +204,15 @@ int df_flow_logpdf_sum(df_chain* chain, const float* x, const float* theta_raw,
  * weight (out×in column-major) then bias; NormalizationLayer: none), the
  * Adam state and the gradient buffer, and rewrites the chain's packed
  * weights after every update, so df_chain_* / df_flow_* calls on the chain
- * see the trained parameters.  Supported: chains whose conditioners all have
- * coupling layers whose conditioners have >= 2 Denses of width <= 256 (the
- * default _dflt_net shape, src/Layers.jl:33-50, with any n_sublayers, e.g. the
- * hidden-256 config-5 model) and σ in {identity, relu, tanh, sigmoid}.
- * Conditioners of the hidden <= 64, <= 4-output default shape run one fused
- * kernel per net; the rest run the layer-wise MFMA path.  Other chains return
- * DF_ERR_UNSUPPORTED. */
+ * see the trained parameters.  Supported: every chain df_chain_create accepts
+ * whose conditioners have >= 2 Denses (width <= 256, any depth, e.g. the
+ * hidden-256 config-5 model), with any of the nine DF_ACT_* activations; σ'
+ * follows NNlib's derivative rules (from the output for relu / tanh_fast /
+ * sigmoid_fast / leakyrelu / elu, from the pre-activation for softplus /
+ * logcosh / swish).  Conditioners of the hidden <= 64, <= 4-output default
+ * shape (_dflt_net, src/Layers.jl:33-50, n_sublayers <= 2) run one fused kernel
+ * per net; the rest run the layer-wise MFMA path.  Single-Dense conditioners
+ * return DF_ERR_UNSUPPORTED. */
 
 typedef struct df_train df_train;
 

@@ -551,6 +551,16 @@ _ACT_GRAD = {
     "relu": lambda x, y: (x > 0).astype(y.dtype),
     "tanh": lambda x, y: 1 - y * y,
     "sigmoid": lambda x, y: y * (1 - y),
+    # NNlib's derivative table for the activations Flux broadcasts (NNlib
+    # src/activations.jl, UNARY_ACTS; NNlib is not vendored, restated from its
+    # published rules): softplus → sigmoid_fast(x), logcosh → tanh(x),
+    # leakyrelu → ifelse(Ω > 0, 1, 1//100), elu → deriv_elu(Ω) = ifelse(Ω ≥ 0, 1, Ω + α),
+    # swish → Ω + sigmoid_fast(x)·(1 − Ω).  sigmoid_fast is exact sigmoid in fp64.
+    "softplus": lambda x, y: _sigmoid(x),
+    "logcosh": lambda x, y: np.tanh(x),
+    "leakyrelu": lambda x, y: np.where(y > 0, 1.0, 0.01).astype(y.dtype),
+    "elu": lambda x, y: np.where(y >= 0, np.ones_like(y), y + 1),
+    "swish": lambda x, y: y + _sigmoid(x) * (1 - y),
 }
 
 

@@ -323,10 +323,75 @@ def test_train_matches_oracle_steps(cuda):
 
 
 def test_train_unsupported_structures(cuda):
+    """A conditioner of a single Dense has no hidden activation to train through
+    the kernels' Dense chain: refused, never silently handled elsewhere."""
     rng = np.random.default_rng(0)
-    sp = dfa.FlowChain(dfa.CouplingLayer(dfa.RNVPCouplingLayer, 4, 2, σ="softplus", rng=rng))
+    ax = O.coupling_axes(4, [3, 4], n=0)
+    lay = dict(ax, kind="rnvp", s_net=_net(rng, [2, 2], ["identity"]), t_net=_net(rng, [2, 2], ["identity"]))
+    ch = spec_to_element({"kind": "chain", "layers": [lay]})
     with pytest.raises(dfa.UnsupportedError):
-        HIPTrainer(sp.hip(), Adam())
+        HIPTrainer(ch.hip(), Adam())
+
+
+def _net(rng, dims, acts, bias_scale=0.1, out_scale=0.5):
+    """A Flux.Chain of Dense(dims[i], dims[i+1], acts[i]) (glorot W, U(±bias_scale) b)."""
+    net = []
+    for i in range(len(dims) - 1):
+        W = O.glorot_uniform(rng, dims[i + 1], dims[i])
+        if i == len(dims) - 2:
+            W = (W * np.float32(out_scale)).astype(np.float32)
+        b = ((rng.random(dims[i + 1]) * 2 - 1) * bias_scale).astype(np.float32)
+        net.append({"W": W, "b": b, "act": acts[i]})
+    return net
+
+
+OTHER_ACTS = ["softplus", "logcosh", "leakyrelu", "elu", "swish"]
+
+
+@pytest.mark.parametrize("act", OTHER_ACTS)
+def test_gradient_parity_other_activations(cuda, path, act):
+    """Training through softplus / logcosh / leakyrelu / elu / swish conditioners
+    (docs/src/documentation.md:99-105 trains a logcosh t-net): σ' by NNlib's
+    rules — from the output for leakyrelu / elu, from the kept pre-activation for
+    softplus / logcosh / swish — against the finite-difference-pinned oracle
+    (tests/test_oracle.py::test_nll_gradient_other_activations_finite_differences)."""
+    rng = np.random.default_rng(5)
+    spec = {"kind": "chain", "layers": [
+        O.rnvp_layer(rng, O.coupling_axes(5, [1, 2, 3], n=1), hidden=16, act=act, bias_scale=0.1, out_scale=0.5),
+        O.coupling_block(rng, O.coupling_axes_cut(5, 2, n=1), n_sub=1, hidden=32, act=act, bias_scale=0.1,
+                         out_scale=0.5)]}
+    _check_grad(cuda, spec, 5, 1, 1500)
+
+
+def _check_grad(cuda, spec, d, n, B):
+    chain = spec_to_element(spec)
+    tr = HIPTrainer(chain.hip(), Adam())
+    x, th = _inputs(d, n, B)
+    g, lpsum = _gpu_grad(tr, x, th, cuda)
+    loss, ref = O.nll_and_grad(spec, x, th if n else np.zeros((0, B)))
+    ref = _flat_oracle_grads(spec, ref)
+    assert abs(-lpsum / B - loss) <= 1e-5 * max(1.0, abs(loss))
+    worst = 0.0
+    for sl in _tensor_slices(spec):
+        worst = max(worst, close(g[sl], ref[sl], G_RTOL, G_ATOL)[1])
+    assert worst <= 1.0, f"gradient violation ratio {worst}"
+
+
+@pytest.mark.parametrize("out_act", ["identity", "softplus", "elu"])
+def test_gradient_parity_docs_nets(cuda, out_act):
+    """The hand-built conditioners of docs/src/documentation.md:101-104
+    (s: Dense(5,32,sigmoid) → Dense(32,16,relu) → Dense(16,4); t: Dense(5,12,relu)
+    → Dense(12,16,logcosh) → Dense(16,32,relu) → Dense(32,4)) on an 8-d chain with
+    one condition: three hidden Denses select the layer-wise path; the output
+    Dense optionally carries an activation of its own."""
+    rng = np.random.default_rng(6)
+    ax = O.coupling_axes(8, [1, 3, 5, 7], n=1)
+    s_net = _net(rng, [5, 32, 16, 4], ["sigmoid", "relu", out_act])
+    t_net = _net(rng, [5, 12, 16, 32, 4], ["relu", "logcosh", "relu", out_act])
+    spec = {"kind": "chain", "layers": [dict(ax, kind="rnvp", s_net=s_net, t_net=t_net),
+                                        O.rnvp_layer(rng, O.reverse_axes(ax), hidden=16, act="swish",
+                                                     bias_scale=0.1, out_scale=0.5)]}
+    _check_grad(cuda, spec, 8, 1, 1200)
 
 
 def test_data_parallel_train_matches_single(cuda, tmp_path):

@@ -201,6 +201,45 @@ def test_nll_gradient_matches_finite_differences():
     assert worst < 1e-5, worst
 
 
+@pytest.mark.parametrize("act", ["softplus", "logcosh", "leakyrelu", "elu", "swish"])
+def test_nll_gradient_other_activations_finite_differences(act):
+    """NNlib's derivative rules for the activations whose σ' needs the
+    pre-activation (softplus, logcosh, swish) or a branch on the output
+    (leakyrelu, elu), pinned by central finite differences like the chain above."""
+    rng = np.random.default_rng(3)
+    chain = {"kind": "chain", "layers": [
+        O.rnvp_layer(rng, O.coupling_axes(4, [3, 1], n=1), hidden=8, act=act, bias_scale=0.1),
+        O.coupling_block(rng, O.coupling_axes_cut(4, 2, n=1), n_sub=3, hidden=8, act=act, bias_scale=0.1)]}
+    x = rng.standard_normal((4, 9))
+    th = rng.random((1, 9))
+    _, grads = O.nll_and_grad(chain, x, th)
+
+    def loss_of():
+        z, l = O.backward(chain, x, th)
+        return -np.mean(O.mvnormal_logpdf(z) + l)
+
+    worst = 0.0
+    for li, L in enumerate(O._flat_layers(chain)):
+        for net in ("s_net", "t_net"):
+            for k, D in enumerate(L[net]):
+                for key in ("W", "b"):
+                    D[key] = D[key].astype(np.float64)
+                    idxs = [(0, 0), (D["W"].shape[0] - 1, D["W"].shape[1] - 1), (D["W"].shape[0] // 2, 1)] \
+                        if key == "W" else [(0,), (-1,)]
+                    for idx in idxs:
+                        orig = D[key][idx]
+                        h = 1e-5
+                        D[key][idx] = orig + h
+                        lp = loss_of()
+                        D[key][idx] = orig - h
+                        lm = loss_of()
+                        D[key][idx] = orig
+                        fd = (lp - lm) / (2 * h)
+                        g = grads[li][net][k][0 if key == "W" else 1][idx]
+                        worst = max(worst, abs(fd - g) / max(1e-6, abs(fd) + abs(g)))
+    assert worst < 1e-5, worst
+
+
 def test_nll_gradient_sums_over_shards():
     """Per-shard gradients with the mean over the global batch sum to the full one."""
     rng = np.random.default_rng(1)
