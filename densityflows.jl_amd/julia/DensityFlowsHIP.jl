@@ -25,11 +25,13 @@ passed by pointer to the same entry points without copies.
 module DensityFlowsHIP
 
 using DensityFlows
-import DensityFlows: forward, backward, forward!, FlowElement, CouplingLayer, CouplingBlock,
-                     FlowChain, RNVPCouplingLayer, NICECouplingLayer, NormalizationLayer
-import Flux
+import DensityFlows: forward, backward, forward!, train!, FlowElement, CouplingLayer, CouplingBlock,
+                     FlowChain, RNVPCouplingLayer, NICECouplingLayer, NormalizationLayer, Flow, DataArrays
+import Distributions, LinearAlgebra
+import Flux, Optimisers
 
-export HIPFlowChain, HIPTrainer, train_step!, train_step_graph!, trainables, copy_trainables!, hip_flow
+export HIPFlowChain, HIPTrainer, HIPComm, train_step!, train_step_graph!, train_step_dist!, trainables,
+       copy_trainables!, hip_flow, flow_nll
 
 const LIB = get(ENV, "DENSITYFLOWS_HIP_LIB", joinpath(@__DIR__, "..", "libdensityflows_hip.so"))
 const ABI_VERSION = Int32(1)
@@ -82,11 +84,30 @@ function check(rc::Integer, what::AbstractString)
     throw(ErrorException("densityflows_hip [$rc] $msg"))
 end
 
+# Device staging buffers of one handle, grown on demand and reused across calls
+# (a host-array call costs the copies, not four allocations).
+mutable struct Staging
+    ptr::Vector{Ptr{Cvoid}}
+    bytes::Vector{Int}
+end
+Staging(n::Integer) = Staging(fill(C_NULL, n), zeros(Int, n))
+
+function _buf!(st::Staging, i::Integer, bytes::Integer)
+    if st.bytes[i] < bytes
+        st.ptr[i] == C_NULL || _free(st.ptr[i])
+        st.ptr[i] = C_NULL; st.bytes[i] = 0
+        st.ptr[i] = _dev(bytes); st.bytes[i] = max(bytes, 1)
+    end
+    return st.ptr[i]
+end
+_release!(st::Staging) = (foreach(p -> p == C_NULL || _free(p), st.ptr); fill!(st.ptr, C_NULL); fill!(st.bytes, 0))
+
 mutable struct HIPFlowChain <: FlowElement
     handle::Ptr{Cvoid}
     d::Int
     n::Int
     keep::Vector{Any}               # host arrays the descriptor pointed to (until create returns)
+    stage::Staging                  # [y, θ, out, ldj, Σ]
 end
 
 # flatten the chain into (element index, layer) pairs; blocks share an element
@@ -149,8 +170,11 @@ function HIPFlowChain(chain::FlowChain; device::Integer = 0)
         check(ccall((:df_chain_create, LIB), Cint, (Ptr{Ptr{Cvoid}}, Ref{ChainDesc}, Cint),
                     h, desc, device), "df_chain_create")
     end
-    obj = HIPFlowChain(h[], d, max(n, 0), Any[])
-    finalizer(c -> ccall((:df_chain_destroy, LIB), Cint, (Ptr{Cvoid},), c.handle), obj)
+    obj = HIPFlowChain(h[], d, max(n, 0), Any[], Staging(5))
+    finalizer(obj) do c
+        _release!(c.stage)
+        ccall((:df_chain_destroy, LIB), Cint, (Ptr{Cvoid},), c.handle)
+    end
     return obj
 end
 
@@ -171,25 +195,43 @@ function _run(sym::Symbol, c::HIPFlowChain, y::Array{Float32,N}, θ::Array{Float
     @assert size(θ, 1) == c.n "dimensions θ must match (n, dims...) with n number of trained parameters"
     B = prod(size(y)[2:N])
     out = similar(y); ldj = Array{Float32}(undef, size(y)[2:N]...)
-    dy, dθ, dout, dl = _dev(sizeof(y)), _dev(sizeof(θ)), _dev(sizeof(y)), _dev(sizeof(ldj))
-    try
-        _h2d(dy, y); c.n > 0 && _h2d(dθ, θ)
-        check(ccall((sym, LIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
-                    c.handle, dy, c.n > 0 ? dθ : C_NULL, dout, dl, B, C_NULL), String(sym))
-        _d2h(out, dout); _d2h(ldj, dl)
-    finally
-        foreach(_free, (dy, dθ, dout, dl))
-    end
+    dy, dθ = _buf!(c.stage, 1, sizeof(y)), _buf!(c.stage, 2, sizeof(θ))
+    dout, dl = _buf!(c.stage, 3, sizeof(y)), _buf!(c.stage, 4, sizeof(ldj))
+    _h2d(dy, y); c.n > 0 && _h2d(dθ, θ)
+    check(ccall((sym, LIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
+                c.handle, dy, c.n > 0 ? dθ : C_NULL, dout, dl, B, C_NULL), String(sym))
+    _d2h(out, dout); _d2h(ldj, dl)
     return out, ldj
 end
 
 forward(c::HIPFlowChain, z::Array{Float32,N}, θ::Array{Float32,N}) where {N} = _run(:df_chain_forward, c, z, θ)
 backward(c::HIPFlowChain, x::Array{Float32,N}, θ::Array{Float32,N}) where {N} = _run(:df_chain_backward, c, x, θ)
 
+"""forward!(c, z, θ): src/Chains.jl:187-197 — z overwritten by the chain's output
+(df_chain_forward_inplace: one staging buffer, no ldj)."""
 function forward!(c::HIPFlowChain, z::Array{Float32,N}, θ::Array{Float32,N}) where {N}
-    x, _ = _run(:df_chain_forward, c, z, θ)
-    z .= x
+    @assert size(z, 1) == c.d "input must be (d, dims...)"
+    @assert size(θ, 1) == c.n "dimensions θ must match (n, dims...) with n number of trained parameters"
+    B = prod(size(z)[2:N])
+    dz, dθ = _buf!(c.stage, 1, sizeof(z)), _buf!(c.stage, 2, sizeof(θ))
+    _h2d(dz, z); c.n > 0 && _h2d(dθ, θ)
+    check(ccall((:df_chain_forward_inplace, LIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
+                c.handle, dz, c.n > 0 ? dθ : C_NULL, B, C_NULL), "df_chain_forward_inplace")
+    _d2h(z, dz)
     return nothing
+end
+
+"""Σ_j logpdf_j (fp64, on the device) of the chain's inverse pass under MvNormal(0, I):
+the sum src/Flows.jl:352-359 averages.  θ as given (already normalised)."""
+function logpdf_sum(c::HIPFlowChain, x::Array{Float32,N}, θ::Array{Float32,N}) where {N}
+    B = prod(size(x)[2:N])
+    dx, dθ, ds = _buf!(c.stage, 1, sizeof(x)), _buf!(c.stage, 2, sizeof(θ)), _buf!(c.stage, 5, 16)
+    _h2d(dx, x); c.n > 0 && _h2d(dθ, θ)
+    check(ccall((:df_flow_logpdf_sum, LIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
+                c.handle, dx, c.n > 0 ? dθ : C_NULL, ds, B, C_NULL), "df_flow_logpdf_sum")
+    r = Vector{Float64}(undef, 1)
+    _d2h(r, ds)
+    return r[1]
 end
 
 # ---- training: train! (src/Flows.jl:380-445) on the device ----------------------
@@ -204,6 +246,7 @@ mutable struct HIPTrainer
     handle::Ptr{Cvoid}
     chain::HIPFlowChain
     n_params::Int
+    stage::Staging                  # [x, θ, Σ logpdf]
 end
 
 """Optimisers.setup(Adam(η, β, ϵ), model) on the device; the trainer owns the flat trainables."""
@@ -213,23 +256,35 @@ function HIPTrainer(c::HIPFlowChain; eta=1f-3, beta=(0.9f0, 0.999f0), epsilon=1f
                 t, c.handle, AdamDesc(eta, beta[1], beta[2], epsilon)), "df_train_create")
     n = Ref{Int64}(0)
     check(ccall((:df_train_num_params, LIB), Cint, (Ptr{Cvoid}, Ref{Int64}), t[], n), "df_train_num_params")
-    obj = HIPTrainer(t[], c, n[])
-    finalizer(x -> ccall((:df_train_destroy, LIB), Cint, (Ptr{Cvoid},), x.handle), obj)
+    obj = HIPTrainer(t[], c, n[], Staging(3))
+    finalizer(obj) do x
+        _release!(x.stage)
+        ccall((:df_train_destroy, LIB), Cint, (Ptr{Cvoid},), x.handle)
+    end
     return obj
 end
 
-"""One mini-batch step of train! (gradient of loss(backward(m, x, θ)) + Adam update)."""
+"""One mini-batch step of train! (gradient of loss(backward(m, x, θ)) + Adam update).
+Returns the batch loss before the update (−Σ logpdf / B)."""
 function train_step!(t::HIPTrainer, x::Array{Float32,N}, θ::Array{Float32,N}) where {N}
     B = prod(size(x)[2:N])
-    dx, dθ = _dev(sizeof(x)), _dev(max(sizeof(θ), 1))
-    try
-        _h2d(dx, x); t.chain.n > 0 && _h2d(dθ, θ)
-        check(ccall((:df_train_step, LIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Cvoid}),
-                    t.handle, dx, t.chain.n > 0 ? dθ : C_NULL, B, C_NULL, C_NULL), "df_train_step")
-    finally
-        foreach(_free, (dx, dθ))
-    end
-    return nothing
+    dx, dθ, ds = _buf!(t.stage, 1, sizeof(x)), _buf!(t.stage, 2, sizeof(θ)), _buf!(t.stage, 3, 8)
+    _h2d(dx, x); t.chain.n > 0 && _h2d(dθ, θ)
+    rc = ccall((:df_train_step, LIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Cvoid}),
+               t.handle, dx, t.chain.n > 0 ? dθ : C_NULL, B, ds, C_NULL)
+    r = Vector{Float64}(undef, 1)
+    rc == DF_ERR_NONFINITE || check(rc, "df_train_step")
+    _d2h(r, ds)
+    l = Float32(-r[1] / B)
+    rc == DF_ERR_NONFINITE && throw(NonFiniteLoss(l))
+    return l
+end
+
+const DF_ERR_NONFINITE = Cint(-6)
+
+"""The debug check of df_train_step refused an update (NaN / Inf loss)."""
+struct NonFiniteLoss <: Exception
+    loss::Float32
 end
 
 """
@@ -252,6 +307,170 @@ function trainables(t::HIPTrainer)
     check(ccall((:df_train_get_params, LIB), Cint, (Ptr{Cvoid}, Ptr{Float32}, Int64), t.handle, p, t.n_params),
           "df_train_get_params")
     return p
+end
+
+"""
+    set_debug!(t::HIPTrainer, on::Bool)
+
+train!(...; debug = true) (src/Flows.jl:404-409): a NaN / Inf batch loss makes the
+step refuse the Adam update (df_train_set_debug → DF_ERR_NONFINITE).
+"""
+set_debug!(t::HIPTrainer, on::Bool) =
+    check(ccall((:df_train_set_debug, LIB), Cint, (Ptr{Cvoid}, Cint), t.handle, on), "df_train_set_debug")
+
+# ---- multi-GPU: RCCL communicator (df_comm_*), one Julia process per GPU ----------
+mutable struct HIPComm
+    handle::Ptr{Cvoid}
+    rank::Int
+    nranks::Int
+    stage::Staging                  # [{Σ, N}]
+end
+
+"""128 opaque bytes (ncclUniqueId) made on rank 0 and shipped to every rank out of band."""
+function comm_unique_id()
+    id = zeros(UInt8, 128)
+    check(ccall((:df_comm_get_unique_id, LIB), Cint, (Ptr{UInt8},), id), "df_comm_get_unique_id")
+    return id
+end
+
+"""HIPComm(nranks, id, rank; device): ncclCommInitRank over the nranks processes (collective)."""
+function HIPComm(nranks::Integer, id::Vector{UInt8}, rank::Integer; device::Integer = 0)
+    length(id) == 128 || throw(ArgumentError("unique id must be 128 bytes"))
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:df_comm_init_rank, LIB), Cint, (Ptr{Ptr{Cvoid}}, Cint, Ptr{UInt8}, Cint, Cint),
+                h, nranks, id, rank, device), "df_comm_init_rank")
+    obj = HIPComm(h[], rank, nranks, Staging(1))
+    finalizer(obj) do c
+        _release!(c.stage)
+        ccall((:df_comm_destroy, LIB), Cint, (Ptr{Cvoid},), c.handle)
+    end
+    return obj
+end
+
+"""
+    flow_nll(c::HIPFlowChain, comm, x_shard, θ_shard) -> loss
+
+Config 3's sharded NLL, `loss = -mean(logpdf)` (src/Flows.jl:352-359) over the
+union of every rank's shard: df_flow_nll all-reduces {Σ logpdf, N} over RCCL.
+θ as given (already normalised).  `comm = nothing`: this process only.
+"""
+function flow_nll(c::HIPFlowChain, comm::Union{HIPComm,Nothing}, x::Array{Float32,N},
+                  θ::Array{Float32,N}) where {N}
+    B = prod(size(x)[2:N])
+    dx, dθ, ds = _buf!(c.stage, 1, sizeof(x)), _buf!(c.stage, 2, sizeof(θ)), _buf!(c.stage, 5, 16)
+    _h2d(dx, x); c.n > 0 && _h2d(dθ, θ)
+    check(ccall((:df_flow_nll, LIB), Cint,
+                (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Cvoid}),
+                c.handle, comm === nothing ? C_NULL : comm.handle, dx, c.n > 0 ? dθ : C_NULL, B, ds, C_NULL),
+          "df_flow_nll")
+    r = Vector{Float64}(undef, 2)
+    _d2h(r, ds)
+    return Float32(-r[1] / r[2])
+end
+
+"""
+    train_step_dist!(t, comm, x_shard, θ_shard, n_total)
+
+One data-parallel train! step: this rank's gradient with the mean over the global
+batch `n_total`, RCCL all-reduce of ∇ and Σ logpdf, the identical Adam step on
+every rank (df_train_step_dist).  Returns the global batch loss before the update.
+"""
+function train_step_dist!(t::HIPTrainer, comm::HIPComm, x::Array{Float32,N}, θ::Array{Float32,N},
+                          n_total::Integer) where {N}
+    B = prod(size(x)[2:N])
+    dx, dθ, ds = _buf!(t.stage, 1, sizeof(x)), _buf!(t.stage, 2, sizeof(θ)), _buf!(t.stage, 3, 8)
+    _h2d(dx, x); t.chain.n > 0 && _h2d(dθ, θ)
+    rc = ccall((:df_train_step_dist, LIB), Cint,
+               (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Int64, Ptr{Cvoid}, Ptr{Cvoid}),
+               t.handle, comm.handle, dx, t.chain.n > 0 ? dθ : C_NULL, B, n_total, ds, C_NULL)
+    rc == DF_ERR_NONFINITE || check(rc, "df_train_step_dist")
+    r = Vector{Float64}(undef, 1)
+    _d2h(r, ds)
+    l = Float32(-r[1] / n_total)
+    rc == DF_ERR_NONFINITE && throw(NonFiniteLoss(l))
+    return l
+end
+
+# ---- train! drop-in (src/Flows.jl:380-445) ------------------------------------------
+const HIPModel = FlowChain{<:Tuple{HIPFlowChain}}
+
+_adam(rule::Optimisers.Adam) = (Float32(rule.eta), (Float32(rule.beta[1]), Float32(rule.beta[2])),
+                                Float32(rule.epsilon))
+_adam(::Any) = throw(ArgumentError("the device optimiser is Optimisers.Adam"))
+
+function _trainer!(flow::Flow, opt)
+    c = flow.model.layers[1]
+    opt isa HIPTrainer && (opt.chain === c || throw(ArgumentError("trainer of another chain")); return opt)
+    # Optimisers.setup(Adam(η, β, ϵ), flow.model): the rule is the state's only content
+    # the device needs; the trainer (and its moments) lives as long as the chain
+    rule = opt isa Optimisers.AbstractRule ? opt : _state_rule(opt)
+    η, β, ϵ = _adam(rule)
+    key = (η, β, ϵ)
+    t = get!(() -> HIPTrainer(c; eta = η, beta = β, epsilon = ϵ), _TRAINERS, (objectid(c), key))
+    return t
+end
+const _TRAINERS = IdDict{Any,HIPTrainer}()
+
+function _state_rule(state)
+    leaf = nothing
+    Optimisers.fmap(x -> (x isa Optimisers.Leaf && (leaf = x); x), state; exclude = x -> x isa Optimisers.Leaf)
+    leaf === nothing && return Optimisers.Adam()        # setup() of a HIP-wrapped model has no leaves
+    return leaf.rule
+end
+
+"""
+    train!(flow, data, opt; epochs=100, batchsize=64, shuffle=true, verbose=true, debug=false)
+
+src/Flows.jl:380-445 for a Flow whose model is `FlowChain((HIPFlowChain(chain),))`:
+the same DataLoader over `normalized_training_data` (batchsize, partial last batch,
+shuffle), one device step per batch (df_train_step: inverse pass, reverse sweep,
+Adam, weight repack), then the full-set train / valid losses pushed to
+`flow.train_loss` / `flow.valid_loss` per epoch (fp64 device Σ logpdf).  `opt` is
+`Optimisers.setup(Adam(η), flow.model)`, an `Optimisers.Adam` rule or a
+`HIPTrainer`.  `debug`: a NaN/Inf batch loss prints and throws ArgumentError
+before the update (as the reference); a NaN/Inf epoch loss prints and returns
+`(z, ldj)` of that set; returns `(nothing, nothing)` at the end.
+Copy the trained parameters into a Julia model with `copy_trainables!`.
+"""
+function train!(flow::Flow{T,D,N,<:HIPModel}, data::DataArrays{T}, opt; epochs::Int = 100,
+                batchsize::Int = 64, shuffle::Bool = true, verbose::Bool = true, debug::Bool = false) where {T,D,N}
+    flow.base isa Distributions.MvNormal && all(iszero, Distributions.mean(flow.base)) &&
+        Distributions.cov(flow.base) == LinearAlgebra.diagm(ones(T, D)) ||
+        throw(ArgumentError("the device loss is the MvNormal(0, I) base of Flow(model, data)"))
+    c = flow.model.layers[1]
+    t = _trainer!(flow, opt)
+    set_debug!(t, debug)
+    train_data = DensityFlows.normalized_training_data(data, flow.metadata)
+    valid_data = DensityFlows.normalized_validation_data(data, flow.metadata)
+    loader = Flux.DataLoader(train_data; batchsize = batchsize, shuffle = shuffle)
+    setloss(set) = Float32(-logpdf_sum(c, set...) / prod(size(set[1])[2:end]))
+    for _ ∈ 1:epochs
+        for (x_batch, t_batch) ∈ loader
+            try
+                train_step!(t, x_batch, t_batch)
+            catch e
+                e isa NonFiniteLoss || rethrow()
+                z, ldj = backward(c, x_batch, t_batch)
+                println("$(e.loss), $ldj, $z")
+                throw(ArgumentError(""))
+            end
+        end
+        train_loss = setloss(train_data)
+        push!(flow.train_loss, train_loss)
+        if debug && ((train_loss != train_loss) || isinf(train_loss))
+            println("Problem with train loss $train_loss")
+            return backward(c, train_data...)
+        end
+        valid_loss = setloss(valid_data)
+        push!(flow.valid_loss, valid_loss)
+        if debug && ((valid_loss != valid_loss) || isinf(valid_loss))
+            println("Problem with valid loss $valid_loss")
+            return backward(c, valid_data...)
+        end
+        verbose && println("epoch: $(length(flow.train_loss)) | train_loss = $train_loss, valid_loss = $valid_loss")
+    end
+    debug && return nothing, nothing
+    return nothing
 end
 
 """

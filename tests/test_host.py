@@ -172,3 +172,31 @@ def test_comm_entry_points_fail_cleanly_without_a_device():
     assert lib.df_flow_nll(None, None, None, None, 4, None, None) == _lib.DF_ERR_INVALID
     assert lib.df_train_set_debug(None, 1) == _lib.DF_ERR_INVALID
     assert lib.df_chain_set_weights(None, None) == _lib.DF_ERR_INVALID
+
+
+def test_julia_shim_binds_only_declared_symbols():
+    """The Julia ccall shim (never executed here: no Julia toolchain)
+    names only entry points include/densityflows_hip.h declares, with balanced
+    blocks, and covers the ABI's groups (chain passes, flow NLL, training, RCCL)."""
+    import re
+
+    src = open(os.path.join(ROOT, "densityflows.jl_amd", "julia", "DensityFlowsHIP.jl")).read()
+    hdr = open(os.path.join(ROOT, "include", "densityflows_hip.h")).read()
+    declared = set(re.findall(r"\b(df_[a-z0-9_]+)\s*\(", hdr))
+    called = set(re.findall(r"ccall\(\(:?\(?:?(df_[a-z0-9_]+)", src)) | set(re.findall(r":(df_[a-z0-9_]+)", src))
+    assert called, "no ccall found"
+    assert called <= declared, sorted(called - declared)
+    for sym in ("df_chain_forward_inplace", "df_flow_logpdf_sum", "df_flow_nll", "df_train_step",
+                "df_train_step_dist", "df_train_set_debug", "df_comm_init_rank", "df_comm_get_unique_id"):
+        assert sym in called, sym
+    # block balance: every opener (function/struct/if/for/try/begin/do/let/module) has an `end`
+    code = re.sub(r'""".*?"""', "", src, flags=re.S)
+    code = re.sub(r"#=.*?=#", "", code, flags=re.S)
+    code = re.sub(r"#.*", "", code)
+    code = re.sub(r'"(\\.|[^"\\])*"', '""', code)
+    opens = len(re.findall(r"^\s*(?:mutable struct|struct|function|module|if|for|while|try|let|begin)\b",
+                           code, flags=re.M))
+    opens += len(re.findall(r"\bdo\b(?:\s+\w+)?\s*$", code, flags=re.M))
+    opens += len(re.findall(r"\bbegin\s*$", code, flags=re.M)) - len(re.findall(r"^\s*begin\s*$", code, flags=re.M))
+    ends = len(re.findall(r"(?<![:\[])\bend\b(?!\s*\])", code))  # not an index `a[2:end]`
+    assert opens == ends, (opens, ends)
