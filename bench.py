@@ -16,9 +16,12 @@ Rank 0 prints ONE JSON line (bench contract).  Extra objects:
                  bound: 3,212 FLOP/B algorithmic intensity); achieved = 2·ΣMAC
                  per sample × samples per launch ÷ mean launch time from HIP
                  events on the launch stream.
-  cpu_baseline — the oracle's Flux-like fp32 numpy restatement (BLAS sgemm,
-                 unfused op sequence) timed on the host cores on a bounded
-                 sample (rank 0, N=1 only).
+  cpu_baseline — the C++/OpenMP fp32 restatement of the reference's CPU
+                 forward (oracle/cpu_flow.cpp: Flux's unfused Dense order,
+                 register-blocked GEMMs, one sample block per thread), pinned
+                 to the numpy oracle by tests/test_oracle.py, timed on the
+                 host cores on a bounded sample (rank 0, N=1 only); config 1
+                 on its stated B = 4096 batches.
 """
 import argparse
 import json
@@ -37,20 +40,42 @@ PEAK_HBM_GBS = 8000.0
 # HBM bytes per launch of the headline kernel from rocprofv3 PMC counters
 # (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, WRITE_SIZE as is; KiB),
 # measured on the headline workload and committed under profiles/.
-TRAFFIC_PROFILES = {"cfg2": os.path.join("profiles", "r01_v14_pmc_cfg2.txt"),
-                    "cfg4": os.path.join("profiles", "r01_v14_pmc_cfg4.txt")}
+TRAFFIC_PROFILES = {"cfg2": os.path.join("profiles", "r02_pmc_cfg2.txt"),
+                    "cfg4": os.path.join("profiles", "r02_pmc_cfg4.txt")}
 
 
-def pmc_traffic(path):
+def source_sha16():
+    """sha256 over the HIP/C++ sources of the product library and its header:
+    the PMC summaries record the one they profiled (tools/gpu_pmc_round.sh)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "densityflows.jl_amd", "csrc")
+    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h", ".cpp")))
+    for f in files + ["../../include/densityflows_hip.h"]:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_summary(path):
+    """traffic (HBM bytes per dispatch, gfx950 FETCH correction), MFMA busy and
+    the profiled source hash from a committed PMC summary."""
+    out = {"traffic": None, "mfma_busy": None, "source": None}
     try:
         vals = {}
         for line in open(os.path.join(ROOT, path)):
+            if line.startswith("# source sha16"):
+                out["source"] = line.split()[-1]
             parts = line.split()
             if len(parts) == 2 and parts[0] in ("FETCH_SIZE", "WRITE_SIZE"):
                 vals[parts[0]] = float(parts[1].replace(",", ""))
-        return (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+            if line.startswith("MFMA busy fraction"):
+                out["mfma_busy"] = float(parts[-1])
+        out["traffic"] = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
     except Exception:
-        return None
+        pass
+    return out
 
 
 CONFIGS = {
@@ -103,32 +128,53 @@ def build_chain(config="cfg2", seed=2):
     return _init_nets(chain, rng)
 
 
-def cpu_baseline(chain, d, n, seconds=12.0, sample=65536):
-    """Oracle fp32 (Flux-like) forward+logdetJ on host cores, bounded sample."""
-    from oracle import flow_oracle as O
-
+def cpu_model():
     try:
-        from threadpoolctl import threadpool_info
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
-        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("internal_api") == "openblas"]
-                      or [1])
-    except Exception:  # pragma: no cover
-        threads = 1
-    spec = chain.to_spec()
+
+def cpu_baseline(chain, d, n, seconds=12.0, sample=65536):
+    """C++/OpenMP fp32 forward+logdetJ (oracle/cpu_flow.cpp) on the host cores,
+    repeated passes over one `sample`-sample batch for ~`seconds`."""
+    from oracle.cpu_flow import CPUFlow, max_threads
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or max_threads()
+    f = CPUFlow(chain.to_spec(), d, n, np.float32)
     rng = np.random.default_rng(0)
     z = rng.standard_normal((d, sample)).astype(np.float32)
     th = rng.random((n, sample)).astype(np.float32)
-    O.forward(spec, z[:, :1024], th[:, :1024], np.float32)  # warm-up
+    f.forward(z[:, :256], th[:, :256], threads)  # warm-up
     done, t0 = 0, time.perf_counter()
     while True:
-        O.forward(spec, z, th, np.float32)
+        f.forward(z, th, threads)
         done += sample
         el = time.perf_counter() - t0
         if el >= seconds:
             break
     return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": int(threads), "kind": "port",
-            "sample": f"{done} samples ({done // sample} passes of a {sample}-sample batch, "
-                      f"numpy fp32 oracle with OpenBLAS sgemm) in {el:.1f} s"}
+            "cpu_model": cpu_model(),
+            "sample": f"{done} samples ({done // sample} passes of a {sample}-sample batch, C++/OpenMP fp32 "
+                      f"restatement oracle/cpu_flow.cpp, {threads} threads) in {el:.1f} s"}
+
+
+class _stdout_to_stderr:
+    """fd 1 → fd 2 for a block (C-level prints such as RCCL's version banner)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
 
 
 def main():
@@ -164,10 +210,11 @@ def main():
         import torch.distributed as dist
 
         backend = os.environ.get("DF_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        with _stdout_to_stderr():   # RCCL's init banner: stdout carries only the JSON line
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group(backend)
 
     import densityflows_amd as dfa
     from densityflows_amd.hip import HIPChain
@@ -192,7 +239,8 @@ def main():
         # nll / train steps, at every rank count (world 1 included)
         from densityflows_amd.parallel import DFComm
 
-        comm = DFComm(gpu, rank, world)
+        with _stdout_to_stderr():
+            comm = DFComm(gpu, rank, world)
     if args.mode == "forward":
         def step():
             hc.run("forward", zbuf, thbuf, xbuf, ldj, B)
@@ -268,11 +316,12 @@ def main():
         flop = 3.0 * info.flops_per_sample * B
         achieved_tflops = flop / kernel_s / 1e12
 
-    traffic, traffic_src = None, None
+    traffic, traffic_src, pmc = None, None, {}
     default_b = (1 << 18) if args.config == "cfg4" else (1 << 20)
     if args.config in TRAFFIC_PROFILES and args.mode == "forward" and B == default_b:
         traffic_src = TRAFFIC_PROFILES[args.config]
-        traffic = pmc_traffic(traffic_src)
+        pmc = pmc_summary(traffic_src)
+        traffic = pmc["traffic"]
     if rank == 0:
         out = {
             "metric": {"forward": METRIC, "nll": "NLL (inverse+logpdf+Σ, RCCL all-reduce) Msamples/s",
@@ -298,6 +347,10 @@ def main():
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_F32_TFLOPS, 4),
                          "traffic": traffic,
                          "traffic_source": traffic_src if traffic is not None else None,
+                         "mfma_busy": pmc.get("mfma_busy"),
+                         "pmc_source_sha16": pmc.get("source"),
+                         "pmc_matches_benched_source": (pmc.get("source") == source_sha16())
+                         if pmc.get("source") else None,
                          "kernel_ms": round(kernel_s * 1e3, 4),
                          "kernel_ms_scope": "whole step (all launches)" if args.mode == "train" else "one launch",
                          "algorithmic_flop_per_sample": info.flops_per_sample,
@@ -306,7 +359,9 @@ def main():
         if args.config != "cfg2":
             out["metric"] = out["metric"].replace("d=5 8-layer RealNVP", CONFIGS[args.config][2].split(":")[0])
         if world == 1 and not args.no_cpu and args.mode == "forward":
-            out["cpu_baseline"] = cpu_baseline(chain, d, n, seconds=args.cpu_seconds)
+            # config 1 is the reference's CPU case at B = 4096 (BASELINE configs[0])
+            out["cpu_baseline"] = cpu_baseline(chain, d, n, seconds=args.cpu_seconds,
+                                               sample=4096 if args.config == "cfg1" else 65536)
             out["vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
     if args.mode == "nll" and rank == 0:

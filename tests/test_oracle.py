@@ -270,3 +270,61 @@ def test_adam_matches_published_update():
                   eps=np.float32(1e-8))
     np.testing.assert_allclose(p, [1.0 - 1e-3, -2.0 + 1e-3, 3.0 - 1e-3], rtol=0, atol=2e-6)
     assert st[2][0] == np.float32(0.9) * np.float32(0.9)
+
+
+# ---------------------------------------------------------------------------
+# the C++/OpenMP restatement (oracle/cpu_flow.cpp, bench.py's cpu_baseline)
+# ---------------------------------------------------------------------------
+
+def _cpu_flow():
+    import os
+    import subprocess
+
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(here, "oracle", "libcpu_flow.so")):
+        subprocess.run(["make", "-C", os.path.join(here, "oracle")], check=True, capture_output=True)
+    from oracle import cpu_flow
+
+    return cpu_flow
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4"])
+def test_cpu_restatement_matches_oracle(name):
+    """The timed CPU proxy computes what the numpy oracle computes: fp64 mode to
+    1e-12 of the golden fixtures (made by the fp64 oracle), fp32 mode within the
+    fp32 oracle's own distance from them."""
+    C = _cpu_flow()
+    spec, g, meta = G.load(name)
+    d, n = meta["d"], meta["n"]
+    th = g["theta"] if n > 0 else np.zeros((0, meta["B"]))
+    x, l = C.CPUFlow(spec, d, n, np.float64).forward(g["z"].astype(np.float64), th, threads=4)
+    np.testing.assert_allclose(x, g["x_fwd"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(l, g["ldj_fwd"], rtol=1e-12, atol=1e-12)
+    x32, l32 = C.CPUFlow(spec, d, n, np.float32).forward(g["z"], th, threads=4)
+    xo, lo = O.forward(spec, g["z"], th, np.float32)
+    ex = np.max(np.abs(x32 - g["x_fwd"])) / np.max(np.abs(g["x_fwd"]))
+    eo = np.max(np.abs(xo - g["x_fwd"])) / np.max(np.abs(g["x_fwd"]))
+    assert ex <= max(1e-5, 4 * eo), (ex, eo)
+
+
+@pytest.mark.parametrize("act", ["tanh", "sigmoid", "softplus", "logcosh", "leakyrelu", "elu", "swish"])
+def test_cpu_restatement_layer_zoo(act):
+    """NICE, n_sublayers 1/3, a NormalizationLayer and every activation, ragged batch."""
+    C = _cpu_flow()
+    rng = np.random.default_rng(7)
+    nice = O.rnvp_layer(rng, O.coupling_axes(4, [2, 4], n=1), hidden=8, act=act, bias_scale=0.1)
+    nice["kind"] = "nice"
+    del nice["s_net"]
+    spec = {"kind": "chain", "layers": [
+        O.rnvp_layer(rng, O.coupling_axes(4, [3, 1], n=1), hidden=8, act=act, bias_scale=0.1),
+        O.coupling_block(rng, O.coupling_axes_cut(4, 2, n=1), n_sub=3, hidden=12, act=act, bias_scale=0.1),
+        nice,
+        O.rnvp_layer(rng, O.coupling_axes(4, [4], n=1), n_sub=1, hidden=8, act=act, bias_scale=0.1),
+        {"kind": "norm", "x_min": np.array([-2, -1, -3, -1.]), "x_max": np.array([2, 3, 1, 2.]),
+         "alpha": -1.0, "beta": 1.0}]}
+    z = rng.standard_normal((4, 301))
+    th = rng.random((1, 301))
+    x, l = C.CPUFlow(spec, 4, 1, np.float64).forward(z, th, threads=3)
+    xo, lo = O.forward(spec, z, th, np.float64)
+    np.testing.assert_allclose(x, xo, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(l, lo, rtol=1e-12, atol=1e-12)
