@@ -89,6 +89,16 @@ struct LdwArgs {
     int64_t batch;
 };
 
+// One merged launch: up to three dW products (ldw) of net i and, optionally, the
+// couple_bwd front of net i+1 (sweep_kernel, df_ltrain.hip).
+struct SweepJob {
+    LdwArgs w[3];
+    int ws[3];              // staging samples of each product (32 or 64, ldw_staging_samples)
+    int nw;
+    LDenseArgs front;       // couple_bwd arguments of the next net
+    int has_front;
+};
+
 hipError_t launch_ldense(int mt, int in_kind, int epi, const LDenseArgs& a, unsigned grid, size_t lds,
                          hipStream_t st);
 hipError_t ldense_occupancy(int mt, int in_kind, int epi, size_t lds, int* blocks);
@@ -101,6 +111,11 @@ hipError_t set_couple_bwd_lds_limit(size_t lds);
 // conditioner input vcat(θ, u)[axis_nn] → xsave [B][ld_x] (rows >= n_in zero), for dW0
 hipError_t launch_gather_features(const LDenseArgs& a, int rows, hipStream_t st);
 size_t ldw_lds_bytes();
+int ldw_staging_samples(const LdwArgs& a);
+// sweep_kernel instances exist for fronts of hidden width 128 / 256 (ht 8 / 16), mto 1 / 2
+bool sweep_supported(int ht, int mto);
+hipError_t set_sweep_lds_limit(size_t lds);
+hipError_t launch_sweep(int ht, int mto, const SweepJob& j, unsigned grid, size_t lds, hipStream_t st);
 // wave grid and per-wave blocks for a dW of mta × ntb tiles (host helper)
 bool ldw_shape(int mta, int ntb, int* wm, int* bm, int* bn);
 

@@ -293,8 +293,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
 // the B operand of the second (accumulator layout = B layout).  One 16-sample tile
 // per wave per round; both fragment sets resident in LDS.
 template <int HT, int MTO>
-__global__ void __launch_bounds__(kBlockThreads, 1) couple_bwd_kernel(LDenseArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+__device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, int bid, int nb) {
     uint8_t* wo = smem;                         // W_out: [kq < HT][m < MTO]
     uint8_t* wt = smem + HT * MTO * 1024;       // W_outᵀ: [kq < MTO][m < HT]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -312,7 +311,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) couple_bwd_kernel(LDenseArgs
     const bool rnvp = (a.kind == DF_LAYER_RNVP);
     // H of the next tile is loaded while this one is processed (rows of a padding
     // sample read the last sample's; its results are never stored)
-    const int64_t tstride = (int64_t)gridDim.x * kWavesPerBlock;
+    const int64_t tstride = (int64_t)nb * kWavesPerBlock;
     f32x4 hn[HT];
     auto load_h = [&](int64_t tile) {
         int64_t sl = tile * 16 + j;
@@ -322,8 +321,8 @@ __global__ void __launch_bounds__(kBlockThreads, 1) couple_bwd_kernel(LDenseArgs
             hn[kq] = kq < a.nkq ? *reinterpret_cast<const f32x4*>(a.in + sl * a.ld_in + 16 * kq + 4 * g)
                                 : f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    if ((int64_t)blockIdx.x * kWavesPerBlock + wave < ntiles) load_h((int64_t)blockIdx.x * kWavesPerBlock + wave);
-    for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wave; tile < ntiles; tile += tstride) {
+    if ((int64_t)bid * kWavesPerBlock + wave < ntiles) load_h((int64_t)bid * kWavesPerBlock + wave);
+    for (int64_t tile = (int64_t)bid * kWavesPerBlock + wave; tile < ntiles; tile += tstride) {
         const int64_t s = tile * 16 + j;
         const bool valid = s < a.batch;
         f32x4 h[HT];
@@ -409,6 +408,12 @@ __global__ void __launch_bounds__(kBlockThreads, 1) couple_bwd_kernel(LDenseArgs
     }
 }
 
+template <int HT, int MTO>
+__global__ void __launch_bounds__(kBlockThreads, 1) couple_bwd_kernel(LDenseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    couple_body<HT, MTO>(a, smem, blockIdx.x, gridDim.x);
+}
+
 template <int MTO>
 void* couple_bwd_ptr_m(int ht) {
     switch (ht) {
@@ -433,8 +438,7 @@ void* couple_bwd_ptr(int ht, int mto) { return mto == 2 ? couple_bwd_ptr_m<2>(ht
 // at most 2 × 2 blocks per wave, whose stages are otherwise too short to cover the
 // two barriers per step)
 template <int S, int BMX, int BNX>  // BMX × BNX: most 16×16 blocks per wave
-__global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float lsm[];
+__device__ __forceinline__ void ldw_body(const LdwArgs& a, float* lsm, int bid, int nblk) {
     const int MA = 16 * a.mta, NB = 16 * a.ntb;
     const int SA = MA + 4, SB = NB + 4;
     float* TA = lsm;
@@ -444,8 +448,8 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
     const int wn = kWavesPerBlock / a.wm;
     const int wi = wave % a.wm, wj = wave / a.wm;
     const int m0 = wi * a.bm, n0 = wj * a.bn;  // first row / column tile of this wave
-    const int64_t per = (a.batch + gridDim.x - 1) / gridDim.x;
-    const int64_t s_begin = (int64_t)blockIdx.x * per;
+    const int64_t per = (a.batch + nblk - 1) / nblk;
+    const int64_t s_begin = (int64_t)bid * per;
     const int64_t s_end = (s_begin + per < a.batch) ? s_begin + per : a.batch;
     (void)wn;
 
@@ -525,7 +529,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
         }
     }
 
-    float* dst = a.partial + (int64_t)blockIdx.x * a.p_total;
+    float* dst = a.partial + (int64_t)bid * a.p_total;
 #pragma unroll
     for (int im = 0; im < BMX; ++im) {
         if (im >= a.bm || m0 + im >= a.mta) continue;
@@ -545,6 +549,49 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
             if (g == 0 && a.b_off >= 0 && 16 * ma + j < a.m_true) dst[a.b_off + 16 * ma + j] = v;
         }
     }
+}
+
+template <int S, int BMX, int BNX>
+__global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lsm[];
+    ldw_body<S, BMX, BNX>(a, lsm, blockIdx.x, gridDim.x);
+}
+
+// One merged launch of the sweep: the dW products of net i (each workgroup's
+// split-K share, as ldw_kernel) and the output-Dense/pullback front of net i+1
+// (couple_body, which depends only on z̄ after net i's W1ᵀδ1 kernel).  Even
+// workgroups run the front first, odd ones the dW products first, so the
+// HBM-bound front of one half of the CUs runs beside the MFMA-bound dW1 of the other
+// half instead of after it (and the two narrow, HBM-bound dW products likewise).
+template <int HT, int MTO>
+__global__ void __launch_bounds__(kBlockThreads, 1) sweep_kernel(SweepJob j) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const bool front_first = HT > 0 && j.has_front && (blockIdx.x & 1) == 0;
+    if constexpr (HT > 0) {
+        if (front_first) {
+            couple_body<HT, MTO>(j.front, smem, blockIdx.x, gridDim.x);
+            __syncthreads();
+        }
+    }
+    for (int k = 0; k < j.nw; ++k) {
+        if (j.ws[k] == 64)
+            ldw_body<64, 2, 2>(j.w[k], reinterpret_cast<float*>(smem), blockIdx.x, gridDim.x);
+        else
+            ldw_body<32, kLdwBM, kLdwBN>(j.w[k], reinterpret_cast<float*>(smem), blockIdx.x, gridDim.x);
+        __syncthreads();
+    }
+    if constexpr (HT > 0) {
+        if (j.has_front && !front_first) couple_body<HT, MTO>(j.front, smem, blockIdx.x, gridDim.x);
+    }
+}
+
+void* sweep_ptr(int ht, int mto) {
+    if (ht == 0) return reinterpret_cast<void*>(&sweep_kernel<0, 1>);
+    if (ht == 16) return mto == 2 ? reinterpret_cast<void*>(&sweep_kernel<16, 2>)
+                                  : reinterpret_cast<void*>(&sweep_kernel<16, 1>);
+    if (ht == 8) return mto == 2 ? reinterpret_cast<void*>(&sweep_kernel<8, 2>)
+                                 : reinterpret_cast<void*>(&sweep_kernel<8, 1>);
+    return nullptr;
 }
 
 // One thread per 4 consecutive features of a sample (rows is a multiple of 16): one
@@ -666,6 +713,27 @@ bool ldw_shape(int mta, int ntb, int* wm, int* bm, int* bn) {
         }
     }
     return ok;
+}
+
+int ldw_staging_samples(const LdwArgs& a) { return ldw_samples(a); }
+
+bool sweep_supported(int ht, int mto) { return sweep_ptr(ht, mto) != nullptr; }
+
+hipError_t set_sweep_lds_limit(size_t lds) {
+    for (int ht : {0, 8, 16})
+        for (int mto : {1, 2}) {
+            hipError_t e = hipFuncSetAttribute(sweep_ptr(ht, mto), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)lds);
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
+
+hipError_t launch_sweep(int ht, int mto, const SweepJob& j, unsigned grid, size_t lds, hipStream_t st) {
+    void* k = sweep_ptr(j.has_front ? ht : 0, mto);
+    if (!k) return hipErrorInvalidValue;
+    void* args[] = {const_cast<SweepJob*>(&j)};
+    return hipLaunchKernel(k, dim3(grid), dim3(kBlockThreads), args, lds, st);
 }
 
 hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st) {

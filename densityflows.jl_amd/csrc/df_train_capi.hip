@@ -124,7 +124,8 @@ struct df_train {
     std::vector<float*> d_lh, d_ld; // H_k and δ_k buffers [cap][lwidth]
     std::vector<float*> d_lv;       // σ'(x_k) buffers [cap][lwidth] (nets with LNet::pre)
     bool any_pre = false;
-    float* d_ly = nullptr;           // ȳ  [cap][lwidth]
+    float* d_lyp[2] = {nullptr, nullptr};  // ȳ  [cap][lwidth], by net parity
+    float* d_lbp[2] = {nullptr, nullptr};  // δ of the last hidden Dense [cap][lwidth], by net parity
     float* d_lx = nullptr;           // gathered conditioner input [cap][lwidth]
     // hidden activations kept by the inverse pass (generic kernel): the sweep then
     // skips the forward recompute.  [(layer·2 + net)·lmax_h + k][B][lwidth]
@@ -153,7 +154,7 @@ void free_all(df_train* t) {
     t->d_bt = nullptr;
     void* ptrs[] = {t->d_params, t->d_m,    t->d_v,    t->d_grad, t->d_partial, t->d_tblob, t->d_pdst,
                     t->d_psrc,   t->d_tdst, t->d_tsrc, t->d_snap, t->d_zbar,    t->d_ebuf,  t->d_lpsum,
-                    t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_ly,   t->d_lx,      t->d_hsave,
+                    t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_lyp[0], t->d_lyp[1], t->d_lbp[0], t->d_lbp[1], t->d_lx, t->d_hsave,
                     t->d_wdst,   t->d_wsrc, t->d_wbdst, t->d_wbsrc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -368,7 +369,7 @@ int ensure_capacity(df_train* t, int64_t batch) {
         }
     t->cap = 0;
     const int64_t cap = std::max<int64_t>(batch, 1024);
-    for (float** p : {&t->d_ly, &t->d_lx, &t->d_hsave})
+    for (float** p : {&t->d_lyp[0], &t->d_lyp[1], &t->d_lbp[0], &t->d_lbp[1], &t->d_lx, &t->d_hsave})
         if (*p) {
             (void)hipFree(*p);
             *p = nullptr;
@@ -385,7 +386,10 @@ int ensure_capacity(df_train* t, int64_t batch) {
         return set_err(DF_ERR_NOMEM, "hipMalloc failed (training activations)");
     if (t->layerwise) {
         const size_t row = sizeof(float) * (size_t)cap * t->lwidth;
-        if (hipMalloc(reinterpret_cast<void**>(&t->d_ly), row) != hipSuccess ||
+        if (hipMalloc(reinterpret_cast<void**>(&t->d_lyp[0]), row) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&t->d_lyp[1]), row) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&t->d_lbp[0]), row) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&t->d_lbp[1]), row) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&t->d_lx), row) != hipSuccess)
             return set_err(DF_ERR_NOMEM, "hipMalloc failed (training activations)");
         // keep the inverse pass's hidden activations when the chain runs on the generic
@@ -463,16 +467,12 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         const size_t lds = (size_t)(nchunks > 1 ? 2 : 1) * std::min(op.nkq, op.chunk_kq) * op.mt * 1024;
         if (e == hipSuccess) e = launch_ldense(op.mt, in_kind, epi, a, dgrid, lds, st);
     };
-    for (const SweepOp& op : t->ops) {
+    // Per net op: base arguments, and whether its backward front is the fused
+    // couple_bwd kernel (kept activations, <= 32 outputs, hidden <= 256).
+    const size_t nops = t->ops.size();
+    auto base_args = [&](const SweepOp& op) {
         const DevLayer& L = P.layers[op.layer];
-        if (op.net < 0) {
-            const float* xmn = static_cast<const float*>(c->d_params) + L.norm_off;
-            e = launch_norm_adjoint(t->d_zbar, xmn, xmn + P.d, L.alpha, L.beta, P.d, batch, st);
-            if (e != hipSuccess) return hip_err(e, "norm adjoint launch");
-            continue;
-        }
         const LNet& N = t->lnets[op.net];
-        const int nd = (int)N.dn.size();
         LDenseArgs b{};
         b.theta = theta;
         b.tmin = flow ? c->d_bounds : nullptr;
@@ -492,21 +492,95 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         b.d = P.d;
         b.n = P.n;
         b.ld_in = b.ld_out = b.ld_h = b.ld_x = W;
-        // H_k: kept by the inverse pass, or recomputed here
+        return b;
+    };
+    const bool no_fuse = std::getenv("DF_TRAIN_NOFUSE") && std::getenv("DF_TRAIN_NOFUSE")[0] == '1';
+    const bool no_merge = std::getenv("DF_TRAIN_NOMERGE") && std::getenv("DF_TRAIN_NOMERGE")[0] == '1';
+    auto keeps = [&](const SweepOp& op) { return t->hsave_on && !t->lnets[op.net].pre; };
+    auto fused_front = [&](const SweepOp& op) {
+        const LNet& N = t->lnets[op.net];
+        const int nd = (int)N.dn.size();
+        return keeps(op) && N.dn[nd - 1].fwd.mt <= 2 && N.dn[0].bwd.mt <= 4 && !no_fuse;
+    };
+    // H_k of a net: kept by the inverse pass, or recomputed into the shared buffers
+    auto Hbuf = [&](const SweepOp& op, int k) -> float* {
         const int net_slot = 2 * op.layer + (op.phase == TR_PHASE_T ? 1 : 0);
-        // a net with a pre-activation σ is recomputed here (σ'(x) is stored beside H)
-        const bool keep = t->hsave_on && !N.pre;
-        auto H = [&](int k) -> float* {
-            return keep ? t->d_hsave + ((int64_t)net_slot * t->lmax_h + k) * batch * W : t->d_lh[k];
-        };
+        return keeps(op) ? t->d_hsave + ((int64_t)net_slot * t->lmax_h + k) * batch * W : t->d_lh[k];
+    };
+    // ȳ and the δ of the last hidden Dense alternate between two buffers from net to
+    // net: a merged launch writes net i+1's while net i's dW products read net i's
+    auto ybuf = [&](int par) { return t->d_lyp[par]; };
+    auto dbuf = [&](const SweepOp& op, int k, int par) -> float* {
+        return k == (int)t->lnets[op.net].dn.size() - 2 ? t->d_lbp[par] : t->d_ld[k];
+    };
+    // couple_bwd: output Dense + pullback → ȳ, then δ_last = (W_outᵀ ȳ) ⊙ σ'(H)
+    auto front_args = [&](const SweepOp& op, int par, LDenseArgs& a, int* ht, int* mto, size_t* lds) {
+        const LNet& N = t->lnets[op.net];
+        const int nd = (int)N.dn.size();
+        const LDense& DO = N.dn[nd - 1];
+        a = base_args(op);
+        a.act = DO.act;
+        a.in = Hbuf(op, nd - 2);
+        a.wfrag = lb + DO.fwd.frag;
+        a.bias = DO.fwd.bias >= 0 ? lbf + DO.fwd.bias : nullptr;
+        a.nkq = DO.fwd.nkq;
+        a.w2frag = lb + DO.bwd.frag;
+        a.nkq2 = DO.bwd.nkq;
+        a.out = ybuf(par);
+        a.out2 = dbuf(op, nd - 2, par);
+        a.dact = N.dn[nd - 2].act;
+        *ht = DO.bwd.mt;
+        *mto = DO.fwd.mt;
+        *lds = (size_t)2 * DO.bwd.mt * DO.fwd.mt * 1024;
+    };
+    // dW = δ · inᵀ, db = Σ δ of every Dense of a net (per-workgroup partials)
+    auto dw_args = [&](const SweepOp& op, int par, std::vector<LdwArgs>& out) -> int {
+        const LNet& N = t->lnets[op.net];
+        const int nd = (int)N.dn.size();
+        for (int k = 0; k < nd; ++k) {
+            const LDense& D = N.dn[k];
+            LdwArgs w{};
+            w.da = (k + 1 == nd) ? ybuf(par) : dbuf(op, k, par);
+            w.lda = W;
+            w.m_true = D.out_dim;
+            w.mta = D.fwd.mt;
+            w.xb = (k == 0) ? t->d_lx : Hbuf(op, k - 1);
+            w.ldb = W;
+            w.n_true = D.in_dim;
+            w.ntb = D.bwd.mt;
+            w.partial = t->d_partial;
+            w.p_total = t->P;
+            w.w_off = D.w_off;
+            w.b_off = D.b_off;
+            w.batch = batch;
+            if (!ldw_shape(w.mta, w.ntb, &w.wm, &w.bm, &w.bn)) return set_err(DF_ERR_UNSUPPORTED, "dW tiling");
+            out.push_back(w);
+        }
+        return DF_OK;
+    };
+
+    int par = 0;               // buffer parity of the current net
+    bool front_done = false;   // this net's couple_bwd ran in the previous merged launch
+    for (size_t oi = 0; oi < nops; ++oi) {
+        const SweepOp& op = t->ops[oi];
+        const DevLayer& L = P.layers[op.layer];
+        if (op.net < 0) {
+            const float* xmn = static_cast<const float*>(c->d_params) + L.norm_off;
+            e = launch_norm_adjoint(t->d_zbar, xmn, xmn + P.d, L.alpha, L.beta, P.d, batch, st);
+            if (e != hipSuccess) return hip_err(e, "norm adjoint launch");
+            front_done = false;
+            continue;
+        }
+        const LNet& N = t->lnets[op.net];
+        const int nd = (int)N.dn.size();
+        const LDenseArgs b = base_args(op);
+        const bool keep = keeps(op);
+        const bool fused = fused_front(op);
         // σ' argument of Dense k's output: H_k, or the stored σ'(x_k)
         auto DACT = [&](int k, LDenseArgs& a) {
-            a.hprev = N.pre ? t->d_lv[k] : H(k);
+            a.hprev = N.pre ? t->d_lv[k] : Hbuf(op, k);
             a.dact = N.pre ? trn::kDactStored : N.dn[k].act;
         };
-        // fused backward front (needs the kept activations, <= 32 outputs, hidden <= 256)
-        const bool fused = keep && N.dn[nd - 1].fwd.mt <= 2 && N.dn[0].bwd.mt <= 4 &&
-                           !(std::getenv("DF_TRAIN_NOFUSE") && std::getenv("DF_TRAIN_NOFUSE")[0] == '1');
         // forward (recompute): H_k = σ(W_k · in + b_k), then the output Dense + coupling pullback → ȳ
         for (int k = 0; k < nd - (fused ? 1 : 0); ++k) {
             LDenseArgs a = b;
@@ -521,58 +595,51 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             if (k == 0) {
                 a.xsave = t->d_lx;
             } else {
-                a.in = H(k - 1);
+                a.in = Hbuf(op, k - 1);
             }
             if (k + 1 < nd) {
-                a.out = H(k);
+                a.out = Hbuf(op, k);
                 a.dsave = N.pre ? t->d_lv[k] : nullptr;
                 dense(N.dn[k].fwd, k == 0 ? LIN_GATHER : LIN_BUF, LEPI_ACT, a);
             } else {
-                a.out = t->d_ly;
+                a.out = ybuf(par);
                 dense(N.dn[k].fwd, LIN_BUF, LEPI_COUPLE, a);
             }
         }
         // backward: δ_{k-1} = (W_kᵀ δ_k) ⊙ σ'(H_{k-1}); x̄ = W0ᵀ δ_0 → z̄ (identity dims)
-        const float* gcur = t->d_ly;
-        const LDense& DO = N.dn[nd - 1];
+        const float* gcur = ybuf(par);
         if (fused) {
-            // output Dense + pullback + (W_outᵀ ȳ) ⊙ σ'(H) in one pass; the last W_kᵀ
-            // product carries x̄ = W0ᵀ δ0 in its epilogue
-            LDenseArgs a = b;
-            a.act = DO.act;
-            a.in = H(nd - 2);
-            a.wfrag = lb + DO.fwd.frag;
-            a.bias = DO.fwd.bias >= 0 ? lbf + DO.fwd.bias : nullptr;
-            a.nkq = DO.fwd.nkq;
-            a.w2frag = lb + DO.bwd.frag;
-            a.nkq2 = DO.bwd.nkq;
-            a.out = t->d_ly;
-            a.out2 = t->d_ld[nd - 2];
-            a.dact = N.dn[nd - 2].act;
-            const size_t lds = (size_t)2 * DO.bwd.mt * DO.fwd.mt * 1024;
-            if (e == hipSuccess) e = launch_couple_bwd(DO.bwd.mt, DO.fwd.mt, a, dgrid, lds, st);
-            gcur = t->d_ld[nd - 2];
+            // output Dense + pullback + (W_outᵀ ȳ) ⊙ σ'(H) in one pass (unless the previous
+            // merged launch ran it); the last W_kᵀ product carries x̄ = W0ᵀ δ0 in its epilogue
+            if (!front_done) {
+                LDenseArgs a;
+                int ht = 0, mto = 0;
+                size_t lds = 0;
+                front_args(op, par, a, &ht, &mto, &lds);
+                if (e == hipSuccess) e = launch_couple_bwd(ht, mto, a, dgrid, lds, st);
+            }
+            gcur = dbuf(op, nd - 2, par);
             for (int k = nd - 2; k >= 1; --k) {
                 LDenseArgs c2 = b;
                 c2.in = gcur;
                 DACT(k - 1, c2);
-                c2.out = t->d_ld[k - 1];
+                c2.out = dbuf(op, k - 1, par);
                 if (k == 1) {
                     c2.w0t = lb + N.dn[0].bwd.frag;
                     c2.w0t_mt = N.dn[0].bwd.mt;
                     c2.w0t_nkq = N.dn[0].bwd.nkq;
-                    const LOp& op = N.dn[k].bwd;
-                    const int nchunks = (op.nkq + op.chunk_kq - 1) / op.chunk_kq;
-                    const size_t lds2 = (size_t)(nchunks > 1 ? 2 : 1) * std::min(op.nkq, op.chunk_kq) * op.mt * 1024 +
+                    const LOp& lo = N.dn[k].bwd;
+                    const int nchunks = (lo.nkq + lo.chunk_kq - 1) / lo.chunk_kq;
+                    const size_t lds2 = (size_t)(nchunks > 1 ? 2 : 1) * std::min(lo.nkq, lo.chunk_kq) * lo.mt * 1024 +
                                         (size_t)c2.w0t_mt * c2.w0t_nkq * 1024 + 64;  // + z̄ column table
-                    c2.wfrag = lb + op.frag;
-                    c2.nkq = op.nkq;
-                    c2.chunk_kq = op.chunk_kq;
-                    if (e == hipSuccess) e = launch_ldense(op.mt, LIN_BUF, LEPI_DACT_XBAR, c2, dgrid, lds2, st);
+                    c2.wfrag = lb + lo.frag;
+                    c2.nkq = lo.nkq;
+                    c2.chunk_kq = lo.chunk_kq;
+                    if (e == hipSuccess) e = launch_ldense(lo.mt, LIN_BUF, LEPI_DACT_XBAR, c2, dgrid, lds2, st);
                 } else {
                     dense(N.dn[k].bwd, LIN_BUF, LEPI_DACT, c2);
                 }
-                gcur = t->d_ld[k - 1];
+                gcur = dbuf(op, k - 1, par);
             }
             if (nd == 2) {
                 LDenseArgs c3 = b;
@@ -584,9 +651,9 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             LDenseArgs a = b;
             a.in = gcur;
             DACT(k - 1, a);
-            a.out = t->d_ld[k - 1];
+            a.out = dbuf(op, k - 1, par);
             dense(N.dn[k].bwd, LIN_BUF, LEPI_DACT, a);
-            gcur = t->d_ld[k - 1];
+            gcur = dbuf(op, k - 1, par);
         }
         if (!fused) {
             LDenseArgs a = b;
@@ -594,27 +661,50 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             dense(N.dn[0].bwd, LIN_BUF, LEPI_XBAR, a);
         }
         if (e != hipSuccess) return hip_err(e, "layer-wise dense launch");
-        // dW = δ · inᵀ, db = Σ δ (per-workgroup partials)
-        for (int k = 0; k < nd; ++k) {
-            const LDense& D = N.dn[k];
-            LdwArgs w{};
-            w.da = (k + 1 == nd) ? t->d_ly : t->d_ld[k];
-            w.lda = W;
-            w.m_true = D.out_dim;
-            w.mta = D.fwd.mt;
-            w.xb = (k == 0) ? t->d_lx : H(k - 1);
-            w.ldb = W;
-            w.n_true = D.in_dim;
-            w.ntb = D.bwd.mt;
-            w.partial = t->d_partial;
-            w.p_total = t->P;
-            w.w_off = D.w_off;
-            w.b_off = D.b_off;
-            w.batch = batch;
-            if (!ldw_shape(w.mta, w.ntb, &w.wm, &w.bm, &w.bn)) return set_err(DF_ERR_UNSUPPORTED, "dW tiling");
-            e = launch_ldw(w, (unsigned)t->lgrid, st);
-            if (e != hipSuccess) return hip_err(e, "dW kernel launch");
+        // dW products of this net, merged with the next net's front when that net is the
+        // next op and runs the fused front (its front reads only z̄ after this net's
+        // W1ᵀδ1 kernel, the kept H, and writes the other parity's ȳ / δ_last)
+        std::vector<LdwArgs> jobs;
+        int rc = dw_args(op, par, jobs);
+        if (rc != DF_OK) return rc;
+        front_done = false;
+        if (!no_merge && jobs.size() <= 3) {
+            SweepJob j{};
+            // narrow (HBM-bound) products first, the hidden×hidden one last: even
+            // workgroups run them in this order, odd ones in reverse
+            std::stable_sort(jobs.begin(), jobs.end(), [](const LdwArgs& p, const LdwArgs& q) {
+                return ldw_staging_samples(p) > ldw_staging_samples(q);
+            });
+            j.nw = (int)jobs.size();
+            for (int k = 0; k < j.nw; ++k) {
+                j.w[k] = jobs[k];
+                j.ws[k] = ldw_staging_samples(jobs[k]);
+            }
+            int ht = 0, mto = 1;
+            size_t lds = ldw_lds_bytes();
+            if (oi + 1 < nops && t->ops[oi + 1].net >= 0 && fused_front(t->ops[oi + 1])) {
+                size_t flds = 0;
+                int fht = 0, fmto = 0;
+                LDenseArgs fa;
+                front_args(t->ops[oi + 1], par ^ 1, fa, &fht, &fmto, &flds);
+                if (sweep_supported(fht, fmto)) {
+                    j.front = fa;
+                    j.has_front = 1;
+                    ht = fht;
+                    mto = fmto;
+                    lds = std::max(lds, flds);
+                }
+            }
+            e = launch_sweep(ht, mto, j, (unsigned)t->lgrid, lds, st);
+            if (e != hipSuccess) return hip_err(e, "merged sweep launch");
+            front_done = j.has_front != 0;
+        } else {
+            for (const LdwArgs& w : jobs) {
+                e = launch_ldw(w, (unsigned)t->lgrid, st);
+                if (e != hipSuccess) return hip_err(e, "dW kernel launch");
+            }
         }
+        par ^= 1;
     }
     return DF_OK;
 }
@@ -693,6 +783,7 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
     if (t->layerwise) {
         e = set_ldense_lds_limit((size_t)2 * kLChunkBytes + 64 * 1024);
         if (e == hipSuccess) e = set_couple_bwd_lds_limit(64 * 1024);
+        if (e == hipSuccess) e = set_sweep_lds_limit(std::max<size_t>(ldw_lds_bytes(), 64 * 1024));
         if (e != hipSuccess) {
             df_train_destroy(t);
             return hip_err(e, "hipFuncSetAttribute(layer-wise training)");

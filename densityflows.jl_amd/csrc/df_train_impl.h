@@ -151,32 +151,93 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
         for (int q = 0; q < NHT; ++q) gWh[m][q] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
+    // Loop-invariant gather tables of this lane (no dependent table loads per tile):
+    // conditioner feature k = 4r + g of vcat(θ, u)[axis_nn] (kind 0 zero, 1 θ, 2 u,
+    // 3 the folded bias's 1), the x̄ targets f = 4g + r (z̄ columns of identity dims,
+    // -1 otherwise) and the transformed dims (z̄ columns).
+    // Packed: xcode[r] = kind << 8 | offset; zxp8 / afp8 one byte per r (0xff: none).
+    int xcode[4];
+    uint32_t zxp8 = 0, afp8 = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        xcode[r] = 0;
+        if (r < N.ks) {
+            const int slot = a.feat[4 * r + g];
+            if (slot < n) xcode[r] = 1 << 8 | slot;
+            else if (slot < n + d) xcode[r] = 2 << 8 | (slot - n);
+            else if (slot == n + d + 3) xcode[r] = 3 << 8;  // folded first-Dense bias (df_plan.cpp pass 1c)
+        }
+        const int f = 4 * g + r;
+        const int fs = (f < G.n_in) ? a.feat[f] : -1;
+        zxp8 |= (uint32_t)((fs >= n && fs < n + d) ? fs - n : 0xff) << (8 * r);
+        afp8 |= (uint32_t)((r < a.n_af) ? a.af[r] - n : 0xff) << (8 * r);
+    }
+    // per-iteration opaque copies of the tables (refreshed at each tile start): the
+    // compiler must not hoist 64-bit addresses derived from them out of the tile loop
+    // (a dozen pointers held live across the loop spill the accumulators)
+    uint32_t zxl = zxp8, afl = afp8;
+    int xcl[4] = {xcode[0], xcode[1], xcode[2], xcode[3]};
+    auto zxc = [&](int r) { return (int)((zxl >> (8 * r)) & 0xffu); };
+    auto afc = [&](int r) { return (int)((afl >> (8 * r)) & 0xffu); };
+    // A tile's global inputs, each issued ahead of its use with independent
+    // addresses (one memory latency, covered by the MFMA work between issue and use):
+    // raw features at the tile start; z̄ of the transformed dims and u_out of those
+    // dims (s phase) or exp(-s) (t phase) before the hidden Dense; z̄ of the x̄
+    // targets before W1ᵀδ.
+    auto load_x = [&](int64_t s, bool ok, float (&xr)[4]) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int kind = xcl[r] >> 8, off = xcl[r] & 0xff;
+            xr[r] = 0.f;
+            if (ok && kind == 1) xr[r] = a.theta[s * n + off];
+            if (ok && kind == 2) xr[r] = a.u_in[s * d + off];
+        }
+    };
+    auto load_pull = [&](int64_t s, bool ok, float (&zbv)[4], float (&aux)[4]) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            zbv[r] = (ok && afc(r) != 0xff) ? a.zbar[s * d + afc(r)] : 0.f;
+            aux[r] = 1.f;
+            if (ok && afc(r) != 0xff) {
+                if (sph) aux[r] = a.u_out[s * d + afc(r)];
+                else if (rnvp) aux[r] = a.ebuf[s * 4 + r];
+            }
+        }
+    };
+    auto load_zx = [&](int64_t s, bool ok, float (&zxv)[4]) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zxv[r] = (ok && zxc(r) != 0xff) ? a.zbar[s * d + zxc(r)] : 0.f;
+    };
+
     const int64_t ntiles = (a.batch + 15) / 16;
-    for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wave; tile < ntiles;
-         tile += (int64_t)gridDim.x * kWavesPerBlock) {
+    const int64_t tstride = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wave; tile < ntiles; tile += tstride) {
         const int64_t s = tile * 16 + j;
         const bool valid = s < a.batch;
+        zxl = zxp8;
+        afl = afp8;
+        asm volatile("" : "+v"(zxl), "+v"(afl));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            xcl[r] = xcode[r];
+            asm volatile("" : "+v"(xcl[r]));
+        }
+        float xr[4], zbp[4], aux[4], zxp[4];
+        load_x(s, valid, xr);
 
         // ---- conditioner input, features k = 4r + g of vcat(θ, u)[axis_nn] ----
         float xin[1][4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            float v = 0.f;
-            if (r < N.ks && valid) {
-                const int slot = a.feat[4 * r + g];
-                if (slot < n) {
-                    v = a.theta[s * n + slot];
-                    if (a.tmin) {  // normalize_input (Data.jl:213-218)
-                        const float lo = a.tmin[slot], diff = a.tmax[slot] - lo;
-                        v = (diff == 0.f) ? 0.f : (v - lo) / diff;
-                    }
-                } else if (slot < n + d) {
-                    v = a.u_in[s * d + (slot - n)];
-                } else if (slot == n + d + 3) {
-                    v = 1.f;  // folded first-Dense bias (df_plan.cpp pass 1c)
-                }
+            float v = xr[r];
+            const int kind = xcl[r] >> 8;
+            if (kind == 1 && a.tmin) {  // normalize_input (Data.jl:213-218)
+                const int slot = xcl[r] & 0xff;
+                const float lo = a.tmin[slot], diff = a.tmax[slot] - lo;
+                v = (diff == 0.f) ? 0.f : (v - lo) / diff;
             }
-            xin[0][r] = v;
+            if (kind == 3) v = 1.f;
+            xin[0][r] = valid ? v : 0.f;
         }
 
         // ---- forward recompute ----
@@ -190,6 +251,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
         } else {
             uni::bias_act<HT, 1, RELU>(fw + N.off_b0, N.act0, A0, !N.fold0);
         }
+        load_pull(s, valid, zbp, aux);
         if constexpr (NH == 1) {
             uni::dense_hidden<HT, 1>(fw + N.off_h, A0, A1);
             if constexpr (PRE) {
@@ -223,14 +285,13 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
             zb[k] = 0.f;
             ee[k] = 1.f;
             if (k < a.n_af && valid) {
-                const int dim = a.af[k] - n;
-                zb[k] = a.zbar[s * d + dim];
+                zb[k] = zbp[k];
                 if (sph) {
                     ee[k] = expf(-o[0][k]);
-                    dout[k] = -zb[k] * a.u_out[s * d + dim] + a.inv_n;  // s̄ = -z̄_af·z_af - j̄
+                    dout[k] = -zb[k] * aux[k] + a.inv_n;  // s̄ = -z̄_af·z_af - j̄
                 } else {
-                    if (rnvp) ee[k] = a.ebuf[s * 4 + k];
-                    dout[k] = -zb[k] * ee[k];                              // t̄ = -z̄_af·exp(-s)
+                    if (rnvp) ee[k] = aux[k];
+                    dout[k] = -zb[k] * ee[k];             // t̄ = -z̄_af·exp(-s)
                 }
                 if (PRE) {
                     if (N.act_out != DF_ACT_IDENTITY) dout[k] = dout[k] * dfo[k];
@@ -303,6 +364,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
                 for (int ma = 0; ma < HT; ++ma)
 #pragma unroll
                     for (int mb = 0; mb < HT; ++mb) gWh[ma][mb] = mfma4(fa[ma][q], fb[mb][q], gWh[ma][mb]);
+            load_zx(s, valid, zxp);
             uni::dense_hidden<HT, 1>(tw + G.off_ht, hb, d0);
             if constexpr (PRE) {
 #pragma unroll
@@ -311,6 +373,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
                 mul_act_grad<HT, RELU>(N.act0, A0[0], d0[0]);
             }
         } else {
+            load_zx(s, valid, zxp);
 #pragma unroll
             for (int m = 0; m < HT; ++m) d0[0][m] = hb[0][m];
         }
@@ -340,18 +403,13 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
         }
         if (valid) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int f = 4 * g + r;
-                if (f < G.n_in) {
-                    const int slot = a.feat[f];
-                    if (slot >= n && slot < n + d) a.zbar[s * d + (slot - n)] += xb[r];
-                }
-            }
+            for (int r = 0; r < 4; ++r)
+                if (zxc(r) != 0xff) a.zbar[s * d + zxc(r)] = zxp[r] + xb[r];
         }
         if (!sph && rnvp && g == 0 && valid) {  // ū_af = z̄_af·exp(-s)
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (k < a.n_af) a.zbar[s * d + (a.af[k] - n)] = zb[k] * ee[k];
+                if (afc(k) != 0xff) a.zbar[s * d + afc(k)] = zb[k] * ee[k];
         }
         lds_order();
     }

@@ -184,6 +184,22 @@ def test_gradient_parity_layerwise_wide(cuda, monkeypatch, name, B, recompute):
     test_gradient_parity(cuda, "layerwise", name, B)
 
 
+@pytest.mark.parametrize("name,B", [("wide", 3001), ("cfg5", 777)])
+def test_merged_sweep_bitwise_equals_separate_launches(cuda, monkeypatch, name, B):
+    """The merged sweep launches (net i's dW products beside net i+1's output-Dense /
+    pullback front, sweep_kernel) compute bitwise the gradient of the separate
+    couple_bwd / ldw launches (DF_TRAIN_NOMERGE=1): same sums in the same order."""
+    spec, chain, d, n = _setup(name)
+    x, th = _inputs(d, n, B)
+    out = []
+    for nomerge in ("0", "1"):
+        monkeypatch.setenv("DF_TRAIN_NOMERGE", nomerge)
+        tr = HIPTrainer(spec_to_element(spec).hip(), Adam())
+        out.append(_gpu_grad(tr, x, th, cuda))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
+
+
 @pytest.mark.parametrize("name", ["cfg2", "wide"])
 def test_gradient_bitwise_reproducible(cuda, path, name):
     spec, chain, d, n = _setup(name)
