@@ -210,11 +210,13 @@ void build_wide(const df_chain_desc* desc, Plan& P) {
                                     put(b, ((int64_t)(kq * N.mto + m) * 64 + lane) * 4 + r, 2, 16 * m + (lane & 15),
                                         16 * kq + 4 * (lane >> 4) + r);
                 }
+                // every wide Dense gets a bias row (zeros without a bias: the kernel adds it
+                // unconditionally, no per-element select; x + 0 = x up to the sign of a zero)
                 auto bias = [&](int dense, int rows) -> int32_t {
                     const df_dense_desc& D = net[dense];
-                    if (!D.b) return -1;
                     const int32_t off = (int32_t)P.wbias.size();
                     P.wbias.resize(P.wbias.size() + rows, 0.f);
+                    if (!D.b) return off;
                     for (int r = 0; r < D.out_dim; ++r) {
                         P.wbias[off + r] = D.b[r];
                         P.wbias_dst.push_back(off + r);

@@ -138,11 +138,10 @@ __device__ __forceinline__ void bias_act(const float* b, int act, const f32x4 (&
     const int g = (threadIdx.x & 63) >> 4;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
-        const f32x4 bb = b ? bias4(b, m) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 bb = bias4(b, m);  // always present (zeros without a bias, df_plan.cpp)
 #pragma unroll
         for (int t = 0; t < T; ++t) {
-            f32x4 v = acc[t][m];
-            if (b) v = v + bb;
+            f32x4 v = acc[t][m] + bb;
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = uni::relu_fast(v[r]);  // planner: σ0 = σ1 = relu
             h[t][m] = v;
@@ -199,7 +198,7 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
             }
         }
     }
-    bias_act(N.b0 >= 0 ? a.wbias + N.b0 : nullptr, N.act0, acc, h);
+    bias_act(a.wbias + N.b0, N.act0, acc, h);
 
     // ---- hidden Dense 256×256: 8 stages of 2 k-quads (chains start from an inline 0) ----
 #pragma unroll
@@ -243,7 +242,7 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
             for (int mm = 0; mm < 4; ++mm) wc[mm] = wn[mm];
         }
     }
-    bias_act(N.b1 >= 0 ? a.wbias + N.b1 : nullptr, N.act1, acc, h);
+    bias_act(a.wbias + N.b1, N.act1, acc, h);
 
     // ---- output Dense (<= 32 outputs): [kq < 16][m < mto] ----
     ensure(N.stage0 + N.nst0 + 8, sg, a);
@@ -286,13 +285,9 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
         if (m < N.mto) {
-            const f32x4 bb = (N.bo >= 0) ? bias4(a.wbias + N.bo, m) : f32x4{0.f, 0.f, 0.f, 0.f};
+            const f32x4 bb = bias4(a.wbias + N.bo, m);
 #pragma unroll
-            for (int t = 0; t < T; ++t) {
-                f32x4 v = out[t][m];
-                if (N.bo >= 0) v = v + bb;  // planner: σo = identity
-                out[t][m] = v;
-            }
+            for (int t = 0; t < T; ++t) out[t][m] = out[t][m] + bb;  // planner: σo = identity
         }
     }
 }
