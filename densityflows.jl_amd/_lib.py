@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdensityflows_hip.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # df_status
 DF_OK = 0
@@ -95,7 +95,8 @@ class df_chain_info(C.Structure):
     _fields_ = [("d", C.c_int32), ("n", C.c_int32), ("n_layers", C.c_int32),
                 ("hidden_tiles", C.c_int32), ("samples_per_block", C.c_int32),
                 ("n_stages", C.c_int32), ("n_params", C.c_int64),
-                ("flops_per_sample", C.c_double), ("weight_bytes", C.c_int64)]
+                ("flops_per_sample", C.c_double), ("weight_bytes", C.c_int64),
+                ("kernel", C.c_int32), ("reserved", C.c_int32), ("split_flops_per_sample", C.c_double)]
 
 
 class df_adam(C.Structure):

@@ -40,32 +40,45 @@ const char* last_error() { return g_err.c_str(); }
 
 using namespace df::api;
 
-static size_t lds_for_tiles(const df_chain* c, int t);
+static size_t lds_for_tiles(const df_chain* c, int t, bool split);
 
-static int uniform_variant(const df::Plan& P) { return P.uniform ? (P.fast ? 3 : P.relu_only ? 2 : 1) : 0; }
+static int uniform_variant(const df::Plan& P, bool split = false) {
+    return P.uniform ? (P.fast ? (split ? 4 : 3) : P.relu_only ? 2 : 1) : 0;
+}
 
-static size_t lds_for_tiles(const df_chain* c, int t) {
+bool use_split(const df_chain* c) {
+    if (!c->plan.split) return false;
+    const char* e = std::getenv("DF_F32_EXACT");
+    return !(e && e[0] == '1');
+}
+
+static size_t lds_for_tiles(const df_chain* c, int t, bool split = false) {
     const df::Plan& P = c->plan;
+    if (split)
+        return (size_t)c->sstage_bytes * c->sn_stage_bufs + c->tab_bytes +
+               (size_t)df::kWavesPerBlock * 16 * t * P.stride * 4;
     return (size_t)c->stage_bytes * c->n_stage_bufs + c->tab_bytes +
            (size_t)df::kWavesPerBlock * 16 * t * P.stride * 4;
 }
 
 // Tiles per wave for this launch: balance the grid over the resident
 // workgroup slots (time ~ rounds × (tiles + fixed per-round overhead)).
-static int choose_tiles(const df_chain* c, int mode, int64_t batch) {
+static int choose_tiles(const df_chain* c, int mode, int64_t batch, bool split) {
     const df::Plan& P = c->plan;
+    const int max_t = split ? P.stiles : P.tiles;
+    const int (*occ)[df::kMaxTilesPerWave + 1] = split ? c->socc : c->occ;
     if (const char* e = std::getenv("DF_TILES")) {  // tuning knob: force the tiles per wave
         const int t = std::atoi(e);
         const int step = P.uniform ? P.tile_group : 1;
-        if (t >= 1 && t <= P.tiles && t % step == 0) return t;
+        if (t >= 1 && t <= max_t && t % step == 0) return t;
     }
     int best = P.uniform ? P.tile_group : 1;
     double best_cost = 1e300;
     const int step = P.uniform ? P.tile_group : 1;
-    for (int t = step; t <= P.tiles; t += step) {
+    for (int t = step; t <= max_t; t += step) {
         const int64_t per_block = (int64_t)df::kWavesPerBlock * 16 * t;
         const int64_t nwg = (batch + per_block - 1) / per_block;
-        const int64_t slots = (int64_t)c->n_cu * (c->occ[mode][t] > 0 ? c->occ[mode][t] : 1);
+        const int64_t slots = (int64_t)c->n_cu * (occ[mode][t] > 0 ? occ[mode][t] : 1);
         const int64_t rounds = (nwg + slots - 1) / slots;
         const double cost = (double)rounds * (t + 0.5);
         if (cost <= best_cost) {
@@ -109,7 +122,8 @@ int df_chain_destroy(df_chain* c) {
     DeviceGuard gd(c->device);
     void* ptrs[] = {c->d_layers, c->d_denses, c->d_chunks,  c->d_stages,  c->d_blob,  c->d_tables,
                     c->d_params, c->d_bounds, c->d_partial, c->d_sched,   c->d_ulayers, c->d_wlayers,
-                    c->d_wstages, c->d_wblob, c->d_wbias,  c->d_wsched};
+                    c->d_wstages, c->d_wblob, c->d_wbias,  c->d_wsched, c->d_sblob, c->d_sstages,
+                    c->d_ssched,  c->d_sulayers};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;
@@ -160,6 +174,16 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
             return set_err(rc, m);
         }
     }
+    if (P.split) {
+        std::vector<int32_t> ssched(P.ssched_fwd);
+        ssched.insert(ssched.end(), P.ssched_bwd.begin(), P.ssched_bwd.end());
+        if ((rc = upload(P.sulayers, &c->d_sulayers)) != DF_OK || (rc = upload(P.sstages, &c->d_sstages)) != DF_OK ||
+            (rc = upload(P.sblob, &c->d_sblob)) != DF_OK || (rc = upload(ssched, &c->d_ssched)) != DF_OK) {
+            std::string m = last_error();
+            df_chain_destroy(c);
+            return set_err(rc, m);
+        }
+    }
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->d_bounds), sizeof(float) * (2 * P.n + 4));
     if (e != hipSuccess) {
         df_chain_destroy(c);
@@ -185,7 +209,12 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
             return hip_err(e, "hipFuncSetAttribute(wide)");
         }
     }
-    e = df::set_kernel_lds_limit(P.ht, P.uniform != 0, c->lds);
+    if (P.split) {
+        c->sstage_bytes = P.sstage_max;
+        c->sn_stage_bufs = P.sstages.size() > 1 ? 2 : 1;
+        c->slds = lds_for_tiles(c, P.stiles, true);
+    }
+    e = df::set_kernel_lds_limit(P.ht, P.uniform != 0, std::max(c->lds, c->slds));
     if (e != hipSuccess) {
         df_chain_destroy(c);
         return hip_err(e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
@@ -196,11 +225,19 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
     for (int mode = 0; mode < 4; ++mode)
         for (int t = 1; t <= P.tiles; ++t) {
             int blocks = 1;
-            if (df::kernel_occupancy(P.ht, mode, P.outv != 0, uniform_variant(P), lds_for_tiles(c, t), &blocks) !=
-                    hipSuccess ||
+            if (df::kernel_occupancy(P.ht, mode, P.outv != 0, uniform_variant(P), lds_for_tiles(c, t, false),
+                                     &blocks) != hipSuccess ||
                 blocks < 1)
                 blocks = 1;
             c->occ[mode][t] = blocks;
+        }
+    for (int mode = 0; mode < 4 && P.split; ++mode)
+        for (int t = 1; t <= P.stiles; ++t) {
+            int blocks = 1;
+            if (df::kernel_occupancy(P.ht, mode, true, 4, lds_for_tiles(c, t, true), &blocks) != hipSuccess ||
+                blocks < 1)
+                blocks = 1;
+            c->socc[mode][t] = blocks;
         }
     *out = c;
     return DF_OK;
@@ -216,6 +253,9 @@ static void fill_info(const df::Plan& P, df_chain_info* out) {
     out->n_params = P.n_params;
     out->flops_per_sample = P.flops_per_sample;
     out->weight_bytes = (int64_t)P.blob.size();
+    out->kernel = P.wide ? 5 : P.split ? 4 : uniform_variant(P);
+    out->reserved = 0;
+    out->split_flops_per_sample = P.split ? P.split_flops_per_sample : 0.0;
 }
 
 int df_chain_get_info(const df_chain* c, df_chain_info* out) {
@@ -254,7 +294,8 @@ int df_chain_set_weights(df_chain* c, const df_chain_desc* desc) {
                       P.blob.size() == Q.blob.size() && P.params.size() == Q.params.size() &&
                       P.ulayers.size() == Q.ulayers.size() && P.wlayers.size() == Q.wlayers.size() &&
                       same_bytes(P.wstages, Q.wstages) && P.wblob.size() == Q.wblob.size() &&
-                      P.wbias.size() == Q.wbias.size() && same_bytes(P.pack_dst, Q.pack_dst);
+                      P.wbias.size() == Q.wbias.size() && same_bytes(P.pack_dst, Q.pack_dst) &&
+                      P.split == Q.split && same_bytes(P.sstages, Q.sstages) && P.sblob.size() == Q.sblob.size();
     if (!same) return set_err(DF_ERR_SHAPE, "df_chain_set_weights: the descriptor's structure differs from the chain's");
     for (size_t i = 0; i < P.layers.size(); ++i)
         if (P.layers[i].kind != Q.layers[i].kind || P.layers[i].n_af != Q.layers[i].n_af)
@@ -269,6 +310,8 @@ int df_chain_set_weights(df_chain* c, const df_chain_desc* desc) {
     if (P.wide && ((rc = refresh(P.wlayers, c->d_wlayers)) != DF_OK || (rc = refresh(P.wblob, c->d_wblob)) != DF_OK ||
                    (rc = refresh(P.wbias, c->d_wbias)) != DF_OK))
         return rc;
+    if (P.split && ((rc = refresh(P.sulayers, c->d_sulayers)) != DF_OK || (rc = refresh(P.sblob, c->d_sblob)) != DF_OK))
+        return rc;
     c->plan.layers = P.layers;
     c->plan.ulayers = P.ulayers;
     c->plan.wlayers = P.wlayers;
@@ -276,6 +319,8 @@ int df_chain_set_weights(df_chain* c, const df_chain_desc* desc) {
     c->plan.params.swap(P.params);
     c->plan.wblob.swap(P.wblob);
     c->plan.wbias.swap(P.wbias);
+    c->plan.sulayers = P.sulayers;
+    c->plan.sblob.swap(P.sblob);
     c->plan.trainables.swap(P.trainables);
     return DF_OK;
 }
@@ -325,13 +370,16 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     DeviceGuard gd(c->device);
     if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
     const bool wide = P.wide && !(std::getenv("DF_NO_WIDE") && std::getenv("DF_NO_WIDE")[0] == '1');
-    const int tiles = wide ? df::kWideT : choose_tiles(c, mode, batch);
+    const bool split = !wide && use_split(c);
+    const int tiles = wide ? df::kWideT : choose_tiles(c, mode, batch, split);
     if (const char* dbg = std::getenv("DF_DEBUG_LAUNCH")) {  // tuning aid: the launch shape on stderr
         if (dbg[0] == '1') {
             std::fprintf(stderr, "[df] mode %d batch %lld kernel %s tiles %d (max %d) occupancy:", mode,
                          (long long)batch,
-                         wide ? "wide" : !P.uniform ? "generic" : P.fast ? "uniform-fast" : "uniform", tiles, P.tiles);
-            for (int t = 1; t <= P.tiles; ++t) std::fprintf(stderr, " t%d=%d", t, c->occ[mode][t]);
+                         wide ? "wide" : !P.uniform ? "generic" : split ? "uniform-fast-split" : P.fast ? "uniform-fast" : "uniform",
+                         tiles, split ? P.stiles : P.tiles);
+            for (int t = 1; t <= (split ? P.stiles : P.tiles); ++t)
+                std::fprintf(stderr, " t%d=%d", t, split ? c->socc[mode][t] : c->occ[mode][t]);
             std::fprintf(stderr, "\n");
         }
     }
@@ -398,9 +446,20 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
         a.wlayers = static_cast<const df::WLayer*>(c->d_wlayers);
         a.wbias = static_cast<const float*>(c->d_wbias);
         e = df::launch_wide(mode, a, (unsigned)grid, c->wide_lds, st);
+    } else if (split) {
+        a.blob = static_cast<const uint8_t*>(c->d_sblob);
+        a.stages = static_cast<const df::DevStage*>(c->d_sstages);
+        a.ulayers = static_cast<const df::ULayer*>(c->d_sulayers);
+        a.stage_bytes = c->sstage_bytes;
+        a.n_stage_bufs = c->sn_stage_bufs;
+        a.sched_fwd = static_cast<const int32_t*>(c->d_ssched);
+        a.sched_bwd = a.sched_fwd + P.ssched_fwd.size();
+        a.n_sched_fwd = (int)P.ssched_fwd.size();
+        a.n_sched_bwd = (int)P.ssched_bwd.size();
+        e = df::launch_chain(P.ht, mode, true, 4, a, (unsigned)grid, lds_for_tiles(c, tiles, true), st);
     } else {
-        e = df::launch_chain(P.ht, mode, P.outv != 0, uniform_variant(P), a, (unsigned)grid, lds_for_tiles(c, tiles),
-                             st);
+        e = df::launch_chain(P.ht, mode, P.outv != 0, uniform_variant(P), a, (unsigned)grid,
+                             lds_for_tiles(c, tiles, false), st);
     }
     if (e != hipSuccess) return hip_err(e, "chain kernel launch");
     if (sum_out) {

@@ -45,7 +45,7 @@ hipError_t set_kernel_lds_limit(int ht, bool uniform, size_t lds) {
 
 hipError_t kernel_occupancy(int ht, int mode, bool outv, int uniform, size_t lds, int* blocks) {
     if (uniform) {
-        const int v = (outv ? 1 : 0) | (uniform >= 2 ? 2 : 0) | (uniform == 3 ? 4 : 0);
+        const int v = (outv ? 1 : 0) | (uniform >= 2 ? 2 : 0) | (uniform >= 3 ? 4 : 0) | (uniform == 4 ? 8 : 0);
         switch (ht) {
             case 1: return uniform_occupancy_ht<1>(mode, v, lds, blocks);
             case 2: return uniform_occupancy_ht<2>(mode, v, lds, blocks);
@@ -66,7 +66,7 @@ hipError_t kernel_occupancy(int ht, int mode, bool outv, int uniform, size_t lds
 hipError_t launch_chain(int ht, int mode, bool outv, int uniform, const ChainArgs& a, unsigned grid, size_t lds,
                         hipStream_t st) {
     if (uniform) {
-        const int v = (outv ? 1 : 0) | (uniform >= 2 ? 2 : 0) | (uniform == 3 ? 4 : 0);
+        const int v = (outv ? 1 : 0) | (uniform >= 2 ? 2 : 0) | (uniform >= 3 ? 4 : 0) | (uniform == 4 ? 8 : 0);
         switch (ht) {
             case 1: return launch_uniform_ht<1>(mode, v, a, grid, lds, st);
             case 2: return launch_uniform_ht<2>(mode, v, a, grid, lds, st);

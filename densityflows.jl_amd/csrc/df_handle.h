@@ -43,7 +43,19 @@ struct df_chain {
     void* d_wbias = nullptr;
     void* d_wsched = nullptr;
     size_t wide_lds = 0;
+    // SPLIT variant of the FAST kernel (plan.split): its own blob, stages, schedules, descriptors
+    void* d_sblob = nullptr;
+    void* d_sstages = nullptr;
+    void* d_ssched = nullptr;
+    void* d_sulayers = nullptr;
+    int sstage_bytes = 0;
+    int sn_stage_bufs = 1;
+    size_t slds = 0;
+    int socc[4][df::kMaxTilesPerWave + 1] = {};
 };
+
+// SPLIT launches unless DF_F32_EXACT=1 (read per launch: an A/B knob for tests and benches)
+bool use_split(const df_chain* c);
 
 namespace df {
 namespace api {

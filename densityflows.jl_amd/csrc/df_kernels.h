@@ -67,7 +67,8 @@ hipError_t chain_occupancy_ht(int mode, bool outv, size_t lds, int* blocks);
 
 // Dispatch over the variant (df_common.hip).
 hipError_t set_kernel_lds_limit(int ht, bool uniform, size_t lds);
-// uniform: 0 = generic kernel, 1 = specialised, 2 = specialised relu-only
+// uniform: 0 = generic kernel, 1 = specialised, 2 = specialised relu-only, 3 = FAST,
+// 4 = FAST on the bf16x3 split stages (SPLIT)
 hipError_t launch_chain(int ht, int mode, bool outv, int uniform, const ChainArgs& a, unsigned grid,
                         size_t lds, hipStream_t st);
 hipError_t kernel_occupancy(int ht, int mode, bool outv, int uniform, size_t lds, int* blocks);

@@ -116,6 +116,180 @@ void check_net(const df_dense_desc* net, int nd, int in_dim, int out_dim, const 
     }
 }
 
+// SPLIT packing of a FAST plan (layout: df_plan.h, kSplit*): every net gets the
+// bf16 planes of its first and hidden Dense; nets are packed whole into stages of
+// at most max(one net, 24 KiB) (a chain of <= 64 KiB is one stage).  The split
+// descriptors are the FAST ones with stage ids and offsets into the split blob.
+void build_split(const df_chain_desc* desc, Plan& P, const std::vector<char>& fold) {
+    P.split = 0;
+    if (!P.fast || (P.ht != 2 && P.ht != 4)) return;
+    if (const char* e = std::getenv("DF_F32_EXACT"))
+        if (e[0] == '1') return;
+    const int ht = P.ht, H = 16 * ht;
+    auto net_bytes = [&](int n_out) {
+        return kSplitFirstBytes(ht) + kSplitHiddenBytes(ht) + 4 * H + round_up((n_out * H + 4) * 4, 16);
+    };
+    int total = 0, biggest = 0;
+    for (const ULayer& U : P.ulayers) {
+        if (U.kind == DF_LAYER_NORM) continue;
+        const int b = net_bytes(U.t.n_out) + (U.kind == DF_LAYER_RNVP ? net_bytes(U.s.n_out) : 0);
+        total += b;
+        biggest = std::max(biggest, std::max(net_bytes(U.t.n_out), U.kind == DF_LAYER_RNVP ? net_bytes(U.s.n_out) : 0));
+    }
+    const int cap = total <= kSingleStageCap ? kSingleStageCap : std::max(kStageCap, round_up(biggest, kStageAlign));
+    std::vector<uint8_t>& blob = P.sblob;
+    int cur = -1, used = 0;
+    auto close = [&]() {
+        if (cur < 0) return;
+        used = round_up(used, kStageAlign);
+        blob.resize((size_t)P.sstages[cur].src_off + used, 0);
+        P.sstages[cur].bytes = used;
+        P.sstage_max = std::max(P.sstage_max, used);
+    };
+    auto alloc = [&](int bytes) {
+        if (cur < 0 || used + bytes > cap) {
+            close();
+            cur = (int)P.sstages.size();
+            DevStage s{};
+            s.src_off = (int64_t)blob.size();
+            P.sstages.push_back(s);
+            used = 0;
+        }
+        const int off = used;
+        used += bytes;
+        blob.resize((size_t)P.sstages[cur].src_off + used, 0);
+        return std::make_pair(cur, off);
+    };
+    P.sulayers = P.ulayers;
+    for (int li = 0; li < desc->n_layers; ++li) {
+        const df_layer_desc& L = desc->layers[li];
+        if (L.kind == DF_LAYER_NORM) continue;
+        const DevLayer& DL = P.layers[li];
+        auto pack = [&](const df_dense_desc* net, int d0, UNet* u) {
+            const DevDense &D0 = P.denses[d0], &D1 = P.denses[d0 + 1], &DO = P.denses[d0 + 2];
+            auto [st, off] = alloc(net_bytes(u->n_out));
+            u->stage = st;
+            u->off_w0 = off;
+            u->off_h = off + kSplitFirstBytes(ht);
+            u->off_out = u->off_h + kSplitHiddenBytes(ht) + 4 * H;
+            u->off_b0 = -1;
+            u->hstride = 0;
+            const int64_t base = P.sstages[st].src_off;
+            auto put16 = [&](int64_t at, int32_t src, int plane, float v) {  // at: byte offset in the stage
+                const uint16_t h = bf16_split_plane(v, plane);
+                std::memcpy(&blob[base + at], &h, 2);
+                if (src >= 0) {
+                    P.spack_dst.push_back((int32_t)(base + at));
+                    P.spack_src.push_back(src * 4 + plane);
+                }
+            };
+            auto put32 = [&](int64_t at, int32_t src, float v) {
+                std::memcpy(&blob[base + at], &v, 4);
+                if (src >= 0) {
+                    P.spack_dst.push_back((int32_t)(base + at));
+                    P.spack_src.push_back(src * 4 + 3);
+                }
+            };
+            // first Dense: slots (w0, w0, w1, w0, w1, w2, 0, 0) of W[16m+i, g] (g = 3 folded: the bias)
+            const df_dense_desc& W0 = net[0];
+            static const int kPlaneOfSlot[6] = {0, 0, 1, 0, 1, 2};
+            for (int m = 0; m < ht; ++m)
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int g = lane >> 4, row = 16 * m + (lane & 15);
+                    float v = 0.f;
+                    int32_t src = -1;
+                    if (row < W0.out_dim) {
+                        if (fold[li] && g == 3) {
+                            v = W0.b[row];
+                            src = D0.b_off + row;
+                        } else if (g < W0.in_dim) {
+                            v = W0.W[(size_t)row + (size_t)W0.out_dim * g];
+                            src = D0.w_off + row + W0.out_dim * g;
+                        }
+                    }
+                    for (int e = 0; e < 6; ++e)
+                        put16(u->off_w0 + ((int64_t)m * 64 + lane) * 16 + 2 * e, src, kPlaneOfSlot[e], v);
+                }
+            // hidden Dense planes
+            const df_dense_desc& W1 = net[1];
+            for (int c = 0; c < ht / 2; ++c)
+                for (int m = 0; m < ht; ++m)
+                    for (int p = 0; p < 3; ++p)
+                        for (int lane = 0; lane < 64; ++lane)
+                            for (int e = 0; e < 8; ++e) {
+                                const int g = lane >> 4, row = 16 * m + (lane & 15);
+                                const int k = 32 * c + 16 * (e >> 2) + 4 * g + (e & 3);
+                                const bool ok = row < W1.out_dim && k < W1.in_dim;
+                                put16(u->off_h + ((((int64_t)c * ht + m) * 3 + p) * 64 + lane) * 16 + 2 * e,
+                                      ok ? D1.w_off + row + W1.out_dim * k : -1, p,
+                                      ok ? W1.W[(size_t)row + (size_t)W1.out_dim * k] : 0.f);
+                            }
+            const int64_t hb = u->off_h + kSplitHiddenBytes(ht);
+            for (int row = 0; row < H; ++row) {
+                const bool ok = W1.b && row < W1.out_dim;
+                put32(hb + 4 * row, ok ? D1.b_off + row : -1, ok ? W1.b[row] : 0.f);
+            }
+            // output Dense (VALU GEMV): [o][H] then b[4]
+            const df_dense_desc& W2 = net[2];
+            for (int o = 0; o < W2.out_dim; ++o)
+                for (int k = 0; k < H; ++k) {
+                    const bool ok = k < W2.in_dim;
+                    put32(u->off_out + 4 * ((int64_t)o * H + k), ok ? DO.w_off + o + W2.out_dim * k : -1,
+                          ok ? W2.W[(size_t)o + (size_t)W2.out_dim * k] : 0.f);
+                }
+            for (int o = 0; o < 4; ++o) {
+                const bool ok = W2.b && o < W2.out_dim;
+                put32(u->off_out + 4 * ((int64_t)W2.out_dim * H + o), ok ? DO.b_off + o : -1, ok ? W2.b[o] : 0.f);
+            }
+            P.split_flops_per_sample += 2.0 * (W0.in_dim * W0.out_dim + W1.in_dim * W1.out_dim);
+        };
+        ULayer& U = P.sulayers[li];
+        if (L.kind == DF_LAYER_RNVP) pack(L.s_net, DL.s_dense0, &U.s);
+        pack(L.t_net, DL.t_dense0, &U.t);
+    }
+    close();
+    auto sched = [&](bool fwd) {
+        std::vector<int32_t> out;
+        auto push = [&](int s) {
+            if (out.empty() || out.back() != s) out.push_back(s);
+        };
+        for (int it = 0; it < P.n_layers; ++it) {
+            const ULayer& U = P.sulayers[fwd ? it : P.n_layers - 1 - it];
+            if (U.kind == DF_LAYER_NORM) continue;
+            if (fwd) {
+                if (U.kind == DF_LAYER_RNVP) push(U.s.stage);
+                push(U.t.stage);
+            } else {
+                push(U.t.stage);
+                if (U.kind == DF_LAYER_RNVP) push(U.s.stage);
+            }
+        }
+        return out;
+    };
+    P.ssched_fwd = sched(true);
+    P.ssched_bwd = sched(false);
+    int target = kLdsPerBlockTarget;
+    if (const char* e = std::getenv("DF_SPLIT_LDS_KB")) target = std::max(32, std::atoi(e)) * 1024;
+    const int nbuf = P.sstages.size() > 1 ? 2 : 1;
+    const int fixed = nbuf * P.sstage_max + round_up((int)P.tables.size() * 4, 16);
+    const int per_tile = kWavesPerBlock * 16 * P.stride * 4;
+    int t = 0;
+    while (t < kMaxTilesPerWave && fixed + (t + 1) * per_tile <= target) ++t;
+    t -= t % P.tile_group;
+    if (t < P.tile_group) {  // no room for one tile group next to the split stages: stay on f32
+        P.sulayers.clear();
+        P.sstages.clear();
+        P.sblob.clear();
+        P.spack_dst.clear();
+        P.spack_src.clear();
+        P.split_flops_per_sample = 0.0;
+        return;
+    }
+    P.stiles = t;
+    P.sblob.resize(round_up((int)P.sblob.size(), 16) + 16, 0);
+    P.split = 1;
+}
+
 // Wide-net packing (see WNet).  Leaves P.wide = 0 unless every coupling layer's
 // conditioners are Dense(in <= 64, 256) → Dense(256, 256) → Dense(256, out <= 32).
 void build_wide(const df_chain_desc* desc, Plan& P) {
@@ -812,6 +986,7 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
             P.stage_max = 0;
         }
         P.blob.resize(round_up((int)P.blob.size(), 16) + 16, 0);
+        build_split(desc, P, fold);
         build_wide(desc, P);
         *out = std::move(P);
         return DF_OK;

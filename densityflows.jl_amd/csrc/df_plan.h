@@ -143,6 +143,42 @@ struct DevStage {
     int32_t pad;
 };
 
+// bf16x3 split of an f32 value (the SPLIT variant of the FAST kernel,
+// df_uniform_impl.h): w = p0 + p1 + p2 exactly for every finite w away from the
+// bf16 overflow edge, each plane rounded to nearest-even from the remainder of
+// the previous ones (8 + 8 + 8 significand bits).  Host packing and the device
+// repack kernel use this same integer routine; the kernels split activations
+// with v_cvt_pk_bf16_f32, which rounds the same way.
+#if defined(__HIPCC__)
+#define DF_HD __host__ __device__
+#else
+#define DF_HD
+#endif
+DF_HD inline uint16_t bf16_rne_bits(float f) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);  // NaN stays NaN
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+DF_HD inline float bf16_bits_to_f32(uint16_t h) { return __builtin_bit_cast(float, (uint32_t)h << 16); }
+DF_HD inline uint16_t bf16_split_plane(float w, int plane) {
+    const uint16_t h0 = bf16_rne_bits(w);
+    if (plane == 0) return h0;
+    const float r = w - bf16_bits_to_f32(h0);
+    const uint16_t h1 = bf16_rne_bits(r);
+    if (plane == 1) return h1;
+    return bf16_rne_bits(r - bf16_bits_to_f32(h1));
+}
+// SPLIT stage layout of one FAST net (H = 16·HT, HT = 2 or 4), byte offsets from
+// the net's start:
+//   first Dense  [m < HT][lane][8 bf16]: lane (g, i) holds W[16m+i, g] as the
+//                product slots (w0, w0, w1, w0, w1, w2, 0, 0) (g = 3: the folded bias)
+//   hidden Dense [c < HT/2][m < HT][plane < 3][lane][8 bf16]: lane (g, i) holds
+//                plane p of W1[16m+i, 32c + 16(e>>2) + 4g + (e&3)], e < 8
+//   hidden bias  f32 [16·HT]
+//   output Dense f32 [n_out][16·HT] then b[4] (VALU GEMV, as in the f32 layout)
+constexpr int kSplitFirstBytes(int ht) { return ht * 1024; }
+constexpr int kSplitHiddenBytes(int ht) { return (ht / 2) * ht * 3 * 1024; }
+
 struct Plan {
     int d = 0, n = 0, n_layers = 0;
     int stride = 0;          // floats per sample row of the LDS state tile
@@ -180,7 +216,20 @@ struct Plan {
     std::vector<int32_t> wsched_fwd, wsched_bwd;
     std::vector<int32_t> wpack_dst, wpack_src;   // wblob float index ← trainables index
     std::vector<int32_t> wbias_dst, wbias_src;   // wbias index ← trainables index
+    // SPLIT variant of the FAST kernel: the conditioner GEMMs on bf16 MFMA with
+    // both operands split in three bf16 planes (6 products, f32 accumulation);
+    // its own blob of one-net stages, schedules and descriptors.
+    int split = 0;
+    int stiles = 0;              // resident 16-sample tiles per wave with the split stages
+    int sstage_max = 0;
+    std::vector<ULayer> sulayers;
+    std::vector<DevStage> sstages;
+    std::vector<uint8_t> sblob;
+    std::vector<int32_t> ssched_fwd, ssched_bwd;
+    // sblob byte offset ← trainables index·4 + plane (plane 3: the f32 value itself)
+    std::vector<int32_t> spack_dst, spack_src;
     double flops_per_sample = 0.0;
+    double split_flops_per_sample = 0.0;  // the part of flops_per_sample the SPLIT kernel runs on bf16 MFMA
 };
 
 // Returns DF_OK or a df_status; *err receives a message mirroring the

@@ -89,5 +89,8 @@ hipError_t launch_adam(float* x, const float* g, float* m, float* v, int64_t cou
                        float eps, float* bt, hipStream_t st);
 hipError_t launch_repack(float* blob, const int32_t* dst, const int32_t* src, int64_t count, const float* params,
                          hipStream_t st);
+// SPLIT blob: byte offset dst[i] ← bf16 plane (src[i] & 3) of params[src[i] >> 2] (plane 3: the f32 value)
+hipError_t launch_repack_split(uint8_t* blob, const int32_t* dst, const int32_t* src, int64_t count,
+                               const float* params, hipStream_t st);
 
 }  // namespace df

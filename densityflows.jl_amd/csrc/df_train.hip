@@ -102,6 +102,17 @@ __global__ void repack_kernel(float* blob, const int32_t* dst, const int32_t* sr
     if (i < count) blob[dst[i]] = params[src[i]];
 }
 
+__global__ void repack_split_kernel(uint8_t* blob, const int32_t* dst, const int32_t* src, int64_t count,
+                                    const float* params) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const int32_t code = src[i];
+    const float v = params[code >> 2];
+    const int plane = code & 3;
+    if (plane == 3) *reinterpret_cast<float*>(blob + dst[i]) = v;
+    else *reinterpret_cast<uint16_t*>(blob + dst[i]) = bf16_split_plane(v, plane);
+}
+
 unsigned blocks_for(int64_t count, int threads) { return (unsigned)((count + threads - 1) / threads); }
 
 }  // namespace
@@ -176,6 +187,14 @@ hipError_t launch_repack(float* blob, const int32_t* dst, const int32_t* src, in
                          hipStream_t st) {
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(repack_kernel, dim3(blocks_for(count, 256)), dim3(256), 0, st, blob, dst, src, count, params);
+    return hipGetLastError();
+}
+
+hipError_t launch_repack_split(uint8_t* blob, const int32_t* dst, const int32_t* src, int64_t count,
+                               const float* params, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(repack_split_kernel, dim3(blocks_for(count, 256)), dim3(256), 0, st, blob, dst, src, count,
+                       params);
     return hipGetLastError();
 }
 

@@ -368,13 +368,119 @@ __device__ __forceinline__ void tail(const uint8_t* buf, const UNet& N, const UL
     }
 }
 
+// ---- SPLIT variant: f32 GEMMs on bf16 MFMA (v_mfma_f32_16x16x32_bf16) ----
+// Both operands are split in three bf16 planes, a = a0 + a1 + a2 exactly (RNE
+// remainders, 8+8+8 significand bits; weights by the planner, activations here
+// by v_cvt_pk_bf16_f32), and W·x is accumulated in f32 from the six products
+// w0x0 + w0x1 + w1x0 + w0x2 + w1x1 + w2x0.  The dropped terms are below 2^-26
+// of |w·x| and every product is exact, so the sums carry f32-level error
+// (≈ Σ|w·x|·2^-24, like the exact-f32 MFMA chain) at 16/6 of its MFMA rate.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x4 mfma_bf(const bf16x8& a, const bf16x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// 8 f32 values → their three bf16 planes.
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const __bf16 h = (__bf16)v[e];
+        const float r = v[e] - (float)h;
+        const __bf16 m = (__bf16)r;
+        p0[e] = h;
+        p1[e] = m;
+        p2[e] = (__bf16)(r - (float)m);
+    }
+}
+
+// First Dense of a FAST net (one k-step, bias folded in slot g = 3): lane group g
+// carries feature g's planes in the product slots (x0, x1, x0, x2, x1, x0, 0, 0)
+// against the planner's (w0, w0, w1, w0, w1, w2, 0, 0): one MFMA per m-tile.
+template <int HT, int TT>
+__device__ __forceinline__ void dense_first_split(const uint8_t* buf, const UNet& N, const float (&xin)[TT][4],
+                                                  f32x4 (&acc)[TT][HT]) {
+    const int lane = threadIdx.x & 63;
+    bf16x8 b[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+        const float x = xin[t][0];
+        const __bf16 h = (__bf16)x;
+        const float r = x - (float)h;
+        const __bf16 m = (__bf16)r;
+        const __bf16 l = (__bf16)(r - (float)m);
+        const __bf16 z = (__bf16)0.f;
+        b[t] = bf16x8{h, m, h, l, m, h, z, z};
+    }
+    const uint8_t* wb = buf + N.off_w0 + lane * 16;
+#pragma unroll
+    for (int m = 0; m < HT; ++m) {
+        const bf16x8 w = *reinterpret_cast<const bf16x8*>(wb + m * 1024);
+#pragma unroll
+        for (int t = 0; t < TT; ++t) acc[t][m] = mfma_bf(w, b[t], f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+}
+
+// Hidden H×H Dense: k-chunk c of 32 inputs = accumulator tiles 2c, 2c+1 (lane
+// (g, j): rows 32c + 16(e>>2) + 4g + (e&3) of sample j), split on the fly.
+template <int HT, int TT>
+__device__ __forceinline__ void dense_hidden_split(const uint8_t* wb, const f32x4 (&in)[TT][HT],
+                                                   f32x4 (&out)[TT][HT]) {
+    const int lane = threadIdx.x & 63;
+    wb += lane * 16;
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int m = 0; m < HT; ++m) out[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < HT / 2; ++c) {
+        bf16x8 x[TT][3];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            const float v[8] = {in[t][2 * c][0],     in[t][2 * c][1],     in[t][2 * c][2],     in[t][2 * c][3],
+                                in[t][2 * c + 1][0], in[t][2 * c + 1][1], in[t][2 * c + 1][2], in[t][2 * c + 1][3]};
+            split8(v, x[t][0], x[t][1], x[t][2]);
+        }
+#pragma unroll
+        for (int m = 0; m < HT; ++m) {
+            const uint8_t* f = wb + (c * HT + m) * 3072;
+            const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(f);
+            const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(f + 1024);
+            const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(f + 2048);
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {  // small terms first
+                f32x4 a = out[t][m];
+                a = mfma_bf(w2, x[t][0], a);
+                a = mfma_bf(w1, x[t][1], a);
+                a = mfma_bf(w0, x[t][2], a);
+                a = mfma_bf(w1, x[t][0], a);
+                a = mfma_bf(w0, x[t][1], a);
+                out[t][m] = mfma_bf(w0, x[t][0], a);
+            }
+        }
+    }
+}
+
 // Evaluate net N for TT 16-sample tiles (state rows ro[t]) and apply its
 // coupling phase; sum[t] = Σ_k s_k for s phases (row order).
-template <int HT, int TT, bool OUTV, bool RELU, int PH, bool FAST = false, int NO = 0>
+template <int HT, int TT, bool OUTV, bool RELU, int PH, bool FAST = false, int NO = 0, bool SPLIT = false>
 __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, const ULayer& L, const int32_t* tab,
                                           float* state, const int (&ro)[TT], float (&sum)[TT]) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
     constexpr bool SPH = (PH == impl::PH_S_FWD || PH == impl::PH_S_BWD);
+    if constexpr (SPLIT && FAST && HT >= 2) {
+        float xin[TT][4];
+        const int slot = tab[L.feat_tab + g];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) xin[t][0] = state[ro[t] + slot];
+        f32x4 A[TT][HT], B[TT][HT];
+        dense_first_split<HT, TT>(buf, N, xin, A);
+        bias_act<HT, TT, true>(buf, DF_ACT_RELU, A, false);
+        dense_hidden_split<HT, TT>(buf + N.off_h, A, B);
+        bias_act<HT, TT, true>(buf + N.off_h + (HT / 2) * HT * 3072, DF_ACT_RELU, B);
+        tail<HT, TT, OUTV, RELU, PH, NO>(buf, N, L, tab, state, ro, sum, B);
+        return;
+    }
     // conditioner input: features k = 4r + g of vcat(θ,z)[axis_nn] (zero slot pads)
     float xin[TT][4];
     const int32_t* feat = tab + L.feat_tab;
@@ -421,7 +527,7 @@ __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, con
 #define DF_FAST_WAVES 4
 #endif
 
-template <int HT, int MODE, bool OUTV, bool RELU, bool FAST = false>
+template <int HT, int MODE, bool OUTV, bool RELU, bool FAST = false, bool SPLIT = false>
 __global__ void __launch_bounds__(kBlockThreads, FAST ? DF_FAST_WAVES : DF_UNI_WAVES)
 uniform_kernel(ChainArgs a) {
     using namespace uni;
@@ -521,7 +627,7 @@ uniform_kernel(ChainArgs a) {
                     float ssum[kTT];
 #pragma unroll
                     for (int t = 0; t < kTT; ++t) ro[t] = row0 + (tt + t) * tstep;
-                    net_tiles<HT, kTT, OUTV, RELU, PH, FAST, NO>(buf, N, L, tab, state, ro, ssum);
+                    net_tiles<HT, kTT, OUTV, RELU, PH, FAST, NO, SPLIT>(buf, N, L, tab, state, ro, ssum);
 #pragma unroll
                     for (int t = 0; t < kTT; ++t) {
                         if (sphase) ldj_update(ro[t], sign * ssum[t], first_in_elem, last_in_elem);
@@ -609,10 +715,10 @@ uniform_kernel(ChainArgs a) {
     }
 }
 
-template <int HT, bool RELU, bool FAST = false>
+template <int HT, bool RELU, bool FAST = false, bool SPLIT = false>
 void* uniform_kernel_ptr_r(int mode, bool outv) {
-#define DF_U(M) (outv ? reinterpret_cast<void*>(&uniform_kernel<HT, M, true, RELU, FAST>) \
-                      : reinterpret_cast<void*>(&uniform_kernel<HT, M, false, RELU, FAST>))
+#define DF_U(M) (outv ? reinterpret_cast<void*>(&uniform_kernel<HT, M, true, RELU, FAST, SPLIT>) \
+                      : reinterpret_cast<void*>(&uniform_kernel<HT, M, false, RELU, FAST, SPLIT>))
     switch (mode) {
         case MODE_FWD: return DF_U(MODE_FWD);
         case MODE_FWD_INPLACE: return DF_U(MODE_FWD_INPLACE);
@@ -623,10 +729,15 @@ void* uniform_kernel_ptr_r(int mode, bool outv) {
 }
 
 // variant index: bit 0 = OUTV, bit 1 = RELU, bit 2 = FAST (RELU only: one first-Dense
-// k-step with the bias folded in, chain-wide)
+// k-step with the bias folded in, chain-wide), bit 3 = SPLIT (FAST with OUTV on the
+// bf16x3 split stages; hidden widths 32 and 64)
 template <int HT>
 void* uniform_kernel_ptr(int mode, int variant) {
     const bool outv = variant & 1;
+    if constexpr (HT >= 2) {
+        if ((variant & 8) && (variant & 4) && outv) return uniform_kernel_ptr_r<HT, true, true, true>(mode, true);
+    }
+    if (variant & 8) return nullptr;
     if (variant & 4) return uniform_kernel_ptr_r<HT, true, true>(mode, outv);
     return (variant & 2) ? uniform_kernel_ptr_r<HT, true>(mode, outv) : uniform_kernel_ptr_r<HT, false>(mode, outv);
 }
@@ -640,8 +751,10 @@ hipError_t launch_uniform_ht(int mode, int variant, const ChainArgs& a, unsigned
 template <int HT>
 hipError_t set_uniform_lds_limit_ht(size_t lds) {
     for (int mode = 0; mode < 4; ++mode)
-        for (int v = 0; v < 8; ++v) {
-            hipError_t e = hipFuncSetAttribute(uniform_kernel_ptr<HT>(mode, v),
+        for (int v = 0; v < 16; ++v) {
+            void* k = uniform_kernel_ptr<HT>(mode, v);
+            if (!k) continue;
+            hipError_t e = hipFuncSetAttribute(k,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }

@@ -34,7 +34,7 @@ export HIPFlowChain, HIPTrainer, HIPComm, train_step!, train_step_graph!, train_
        copy_trainables!, hip_flow, flow_nll
 
 const LIB = get(ENV, "DENSITYFLOWS_HIP_LIB", joinpath(@__DIR__, "..", "libdensityflows_hip.so"))
-const ABI_VERSION = Int32(1)
+const ABI_VERSION = Int32(2)
 
 # ---- C structs (include/densityflows_hip.h) --------------------------------
 struct DenseDesc                 # df_dense_desc

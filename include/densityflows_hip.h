@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DF_ABI_VERSION 1
+#define DF_ABI_VERSION 2
 
 typedef enum df_status {
     DF_OK = 0,
@@ -127,6 +127,12 @@ typedef struct df_chain_info {
     int64_t n_params;             /* trainable parameters (Flux.trainables)   */
     double flops_per_sample;      /* 2 × Σ Dense MACs (algorithmic)           */
     int64_t weight_bytes;         /* packed device weight blob                */
+    int32_t kernel;               /* chain-pass kernel: 0 generic, 1 specialised,
+                                     2 specialised relu-only, 3 FAST, 4 FAST on
+                                     bf16x3 split stages (SPLIT), 5 wide       */
+    int32_t reserved;
+    double split_flops_per_sample; /* part of flops_per_sample that kernel 4
+                                      runs as six bf16 products on MFMA      */
 } df_chain_info;
 
 int df_get_abi_version(void);

@@ -135,9 +135,12 @@ def test_folded_bias_bit_identical(cuda, name, monkeypatch):
     """The specialised kernel's FAST variant folds the first Dense's bias into the
     last k-slot of the MFMA chain (df_plan.cpp pass 1c): fma(b, 1, W*x) rounds
     exactly like the separate `W*x .+ b`, so x, ldj and the inverse are bitwise
-    those of the unfolded plan (DF_NO_FOLD=1) and of the non-FAST variant."""
+    those of the unfolded plan (DF_NO_FOLD=1) and of the non-FAST variant.  All three
+    on exact-f32 MFMA (DF_F32_EXACT=1: the SPLIT variant rounds differently, see
+    test_split_variant_accuracy)."""
     spec, g, meta = G.load(name)
     th = _t(g["theta"], cuda) if meta["n"] > 0 else None
+    monkeypatch.setenv("DF_F32_EXACT", "1")
     outs = []
     for env in ({}, {"DF_NO_FAST": "1"}, {"DF_NO_FOLD": "1"}):
         for k in ("DF_NO_FAST", "DF_NO_FOLD"):
@@ -182,11 +185,14 @@ def test_fast_variant_cases(cuda, case, monkeypatch, capfd):
     import bench
 
     outs = []
-    for env in ({"DF_DEBUG_LAUNCH": "1"}, {"DF_NO_FAST": "1"}, {"DF_NO_FOLD": "1"}):
-        for k in ("DF_NO_FAST", "DF_NO_FOLD", "DF_DEBUG_LAUNCH"):
+    for env in ({"DF_DEBUG_LAUNCH": "1"}, {"DF_NO_FAST": "1"}, {"DF_NO_FOLD": "1"}, {"SPLIT": "1"}):
+        for k in ("DF_NO_FAST", "DF_NO_FOLD", "DF_DEBUG_LAUNCH", "DF_F32_EXACT"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
-            monkeypatch.setenv(k, v)
+            if k != "SPLIT":
+                monkeypatch.setenv(k, v)
+        if "SPLIT" not in env:   # bitwise comparisons among the exact-f32 kernels
+            monkeypatch.setenv("DF_F32_EXACT", "1")
         rng = np.random.default_rng(11)
         d, n, chain = _fast_case_chain(case, rng)
         bench._init_nets(chain, rng)      # non-zero biases: the folded slot carries them
@@ -197,6 +203,13 @@ def test_fast_variant_cases(cuda, case, monkeypatch, capfd):
         tth = _t(th, cuda) if n else None
         x, lf = dfa.forward(chain, _t(z, cuda), tth)
         zb, lb = dfa.backward(chain, x, tth)
+        if "SPLIT" in env:   # the bf16x3 SPLIT kernel (hidden 32 / 64): f32-accurate, not bitwise
+            assert _kernel_of(chain) in ((4,) if case in ("af1_h64", "af4_h64", "nice_h32") else
+                                         (3,) if case == "block_h16" else (1, 2))
+            xo, lo = O.forward(chain.to_spec(), z, th if n else np.zeros((0, B), np.float32), np.float64)
+            assert close(_np(x), xo, RTOL)[0] and close(_np(lf), lo, RTOL)[0]
+            assert np.all(np.abs(_np(lf) + _np(lb)) <= 2e-6 + 1e-5 * np.abs(_np(lf)))
+            continue
         outs.append([_np(v) for v in (x, lf, zb, lb)])
         if "DF_DEBUG_LAUNCH" in env:
             import torch
@@ -458,6 +471,61 @@ def strict_rel(a, b, floor=STRICT_FLOOR):
     r = np.abs(a[m] - b[m]) / np.abs(b[m])
     return (float(r.max()), float(np.percentile(r, 99.9)), float(np.percentile(r, 99)),
             float((r > STRICT_RTOL).mean()), int(m.sum()))
+
+
+def _kernel_of(chain):
+    return chain.hip().info.kernel
+
+
+@pytest.mark.parametrize("name", ["cfg2", "fast_h32"])
+def test_split_variant_accuracy(cuda, name, monkeypatch):
+    """The SPLIT variant (df_uniform_impl.h: first and hidden Dense on bf16 MFMA
+    with both operands in three bf16 planes, six products, f32 accumulation) is an
+    f32-accurate evaluation: against the fp64 truth its strict per-element error
+    is within 1.5× that of the exact-f32 MFMA kernel (DF_F32_EXACT=1) at the
+    median and the 99th percentile, for x and ldj in both directions; the worst
+    (ill-conditioned) element within 2× the worst of the exact-f32 kernel and of
+    Flux's op order in fp32."""
+    if name == "cfg2":
+        spec, g, meta = G.load("cfg2")
+        z, xin = g["z"], g["x_in"]
+        xo, lo = g["x_fwd"], g["ldj_fwd"]
+        zo, lbo = g["z_bwd"], g["ldj_bwd"]
+    else:  # hidden 32 (HT = 2), 4 RNVP layers on d = 6
+        rng = np.random.default_rng(7)
+        ch = dfa.FlowChain.repeat(dfa.CouplingBlock, 2, 6, hidden_dim_s=32, hidden_dim_t=32, rng=rng)
+        spec = ch.to_spec()
+        z = rng.standard_normal((6, 3000))
+        xo, lo = O.forward(spec, z, np.zeros((0, 3000)), np.float64)
+        xin = xo.astype(np.float32)
+        zo, lbo = O.backward(spec, xin.astype(np.float64), np.zeros((0, 3000)), np.float64)
+        z = z.astype(np.float32)
+    ref32 = list(O.forward(spec, z, np.zeros((0, z.shape[1]), np.float32), np.float32)) + \
+        list(O.backward(spec, xin, np.zeros((0, z.shape[1]), np.float32), np.float32))
+    res = {}
+    for exact in ("0", "1"):
+        monkeypatch.setenv("DF_F32_EXACT", exact)
+        chain = spec_to_element(spec)
+        assert _kernel_of(chain) == (3 if exact == "1" else 4)
+        x, lf = dfa.forward(chain, _t(z, cuda))
+        zb, lb = dfa.backward(chain, _t(xin, cuda))
+        res[exact] = [_np(v) for v in (x, lf, zb, lb)]
+    print(f"strict relative error vs fp64 ({name}): quantity split(median, p99, max) | exact-f32(same)")
+    for i, (key, truth) in enumerate((("x", xo), ("ldj", lo), ("z", zo), ("ldj_bwd", lbo))):
+        es = strict_rel(res["0"][i], truth)
+        ee = strict_rel(res["1"][i], truth)
+        a = np.abs(np.asarray(truth, np.float64))
+        m = a > 1e-3
+        med_s = float(np.median(np.abs(res["0"][i].astype(np.float64) - truth)[m] / a[m]))
+        med_e = float(np.median(np.abs(res["1"][i].astype(np.float64) - truth)[m] / a[m]))
+        print(f"  {key}: ({med_s:.3g}, {es[2]:.3g}, {es[0]:.3g}) | ({med_e:.3g}, {ee[2]:.3g}, {ee[0]:.3g})")
+        # the worst element is an ill-conditioned sample whose error depends on the
+        # summation order: judged, as in test_strict_elementwise_relative_error, against
+        # 2× the worst of the exact-f32 kernel and of Flux's own op order in fp32
+        ef = strict_rel(ref32[i], truth)
+        assert med_s <= 1.5 * med_e + 1e-8, (key, med_s, med_e)
+        assert es[2] <= 1.5 * ee[2] + 1e-8, (key, es, ee)
+        assert es[0] <= max(1e-5, 2.0 * max(ee[0], ef[0])), (key, es, ee, ef)
 
 
 @pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4"])
