@@ -36,6 +36,12 @@ sys.path.insert(0, ROOT)
 
 METRIC = "forward+logdetJ Msamples/s, d=5 8-layer RealNVP, 1/2/4/8 MI355X"
 PEAK_F32_TFLOPS = 157.3   # MI355X f32 MFMA dense peak (MI355X_MICROARCH.md)
+# SPLIT kernel (df_uniform_impl.h): an f32 product as six bf16 MFMA products; bf16
+# MFMA runs 16x the f32 MFMA rate (MI355X_MICROARCH.md § Matrix cores)
+PEAK_SPLIT_TFLOPS = 16.0 * PEAK_F32_TFLOPS / 6.0
+KERNELS = {0: "generic", 1: "specialised", 2: "specialised relu-only", 3: "FAST (exact f32 MFMA)",
+           4: "FAST SPLIT (bf16x3 planes, 6 products on bf16 MFMA, f32 accumulate)", 5: "wide (exact f32 MFMA)",
+           6: "wide SPLIT (bf16x3 planes, 6 products on bf16 MFMA, f32 accumulate)"}
 PEAK_HBM_GBS = 8000.0
 # HBM bytes per launch of the headline kernel from rocprofv3 PMC counters
 # (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, WRITE_SIZE as is; KiB),
@@ -190,6 +196,8 @@ def main():
                     help="cfg2 is the headline (BASELINE configs[1]); cfg1/cfg4 are secondary measurements")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-exact", action="store_true",
+                    help="skip the exact-f32 FAST kernel timing that accompanies a SPLIT-kernel bench")
     ap.add_argument("--graph", action="store_true",
                     help="train mode, one rank: replay each step as one hipGraph (df_train_step_graph)")
     args = ap.parse_args()
@@ -316,6 +324,37 @@ def main():
         flop = 3.0 * info.flops_per_sample * B
         achieved_tflops = flop / kernel_s / 1e12
 
+    # roofline peak of the arithmetic the kernel runs: the SPLIT kernel computes its
+    # first and hidden Dense GEMMs on bf16 MFMA (six products per f32 product), the
+    # output Dense as an f32 VALU GEMV; every other kernel is exact f32 MFMA
+    kernel_id = int(getattr(info, "kernel", 3))
+    f_split = float(getattr(info, "split_flops_per_sample", 0.0)) if args.mode != "train" else 0.0
+    f_all = float(info.flops_per_sample)
+    peak = PEAK_F32_TFLOPS
+    if f_split > 0.0:
+        peak = f_all / (f_split / PEAK_SPLIT_TFLOPS + (f_all - f_split) / PEAK_F32_TFLOPS)
+
+    exact = None
+    if kernel_id in (4, 6) and args.mode == "forward" and not args.no_exact:
+        # the same launches on the exact-f32 FAST kernel (DF_F32_EXACT is read per launch)
+        os.environ["DF_F32_EXACT"] = "1"
+        for _ in range(min(args.warmup, 20)):
+            step()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        k_exact = max(20, args.steps // 4)
+        e0.record(stream)
+        for _ in range(k_exact):
+            step()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        del os.environ["DF_F32_EXACT"]
+        ms = e0.elapsed_time(e1) / k_exact
+        exact = {"kernel": KERNELS[kernel_id - 1], "ms_per_step": round(ms, 4), "value": round(B * world / ms / 1e3, 3),
+                 "frac_of_f32_peak": round(f_all * B / (ms / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4), "steps": k_exact}
+
     traffic, traffic_src, pmc = None, None, {}
     default_b = (1 << 18) if args.config == "cfg4" else (1 << 20)
     if args.config in TRAFFIC_PROFILES and args.mode == "forward" and B == default_b:
@@ -336,15 +375,20 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32",   # f32 in / f32 out at f32-level error; kernel arithmetic in roofline.kernel
             "data": "synthetic: z ~ N(0,1) generated on device; random-init weights (glorot, see bench.build_chain)",
             "config": {"workload": workload + ("" if world == 1 else f"; config3 sharding {world}x"),
                        "per_gpu_batch": B, "global_batch": B * world,
                        "parallelism": {"forward": f"dp{world} (independent sample shards, no data-path collective)",
                                        "nll": f"dp{world} + RCCL all-reduce of the NLL partial",
                                        "train": f"dp{world} + RCCL all-reduce of the flat gradient"}[args.mode]},
-            "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": PEAK_F32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_F32_TFLOPS, 4),
+            "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": round(peak, 2),
+                         "unit": "TFLOP/s", "frac": round(achieved_tflops / peak, 4),
+                         "kernel": KERNELS.get(kernel_id, str(kernel_id)),
+                         "peak_basis": ("f32 MFMA 157.3 TF" if f_split == 0.0 else
+                                        f"mix: {f_split:.0f} of {f_all:.0f} FLOP/sample at the bf16x3 split rate "
+                                        f"{PEAK_SPLIT_TFLOPS:.1f} TF (bf16 MFMA / 6), the rest at f32 157.3 TF"),
+                         "frac_of_f32_mfma_peak": round(achieved_tflops / PEAK_F32_TFLOPS, 4),
                          "traffic": traffic,
                          "traffic_source": traffic_src if traffic is not None else None,
                          "mfma_busy": pmc.get("mfma_busy"),
@@ -358,6 +402,8 @@ def main():
         }
         if args.config != "cfg2":
             out["metric"] = out["metric"].replace("d=5 8-layer RealNVP", CONFIGS[args.config][2].split(":")[0])
+        if exact is not None:
+            out["f32_exact_kernel"] = exact
         if world == 1 and not args.no_cpu and args.mode == "forward":
             # config 1 is the reference's CPU case at B = 4096 (BASELINE configs[0])
             out["cpu_baseline"] = cpu_baseline(chain, d, n, seconds=args.cpu_seconds,

@@ -52,6 +52,12 @@ bool use_split(const df_chain* c) {
     return !(e && e[0] == '1');
 }
 
+bool use_wsplit(const df_chain* c) {
+    if (!c->plan.wsplit) return false;
+    const char* e = std::getenv("DF_F32_EXACT");
+    return !(e && e[0] == '1');
+}
+
 static size_t lds_for_tiles(const df_chain* c, int t, bool split = false) {
     const df::Plan& P = c->plan;
     if (split)
@@ -123,7 +129,8 @@ int df_chain_destroy(df_chain* c) {
     void* ptrs[] = {c->d_layers, c->d_denses, c->d_chunks,  c->d_stages,  c->d_blob,  c->d_tables,
                     c->d_params, c->d_bounds, c->d_partial, c->d_sched,   c->d_ulayers, c->d_wlayers,
                     c->d_wstages, c->d_wblob, c->d_wbias,  c->d_wsched, c->d_sblob, c->d_sstages,
-                    c->d_ssched,  c->d_sulayers};
+                    c->d_ssched,  c->d_sulayers, c->d_wslayers, c->d_wsstages, c->d_wsblob, c->d_wssched,
+                    c->d_wstables};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;
@@ -184,6 +191,17 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
             return set_err(rc, m);
         }
     }
+    if (P.wsplit) {
+        std::vector<int32_t> wssched(P.wssched_fwd);
+        wssched.insert(wssched.end(), P.wssched_bwd.begin(), P.wssched_bwd.end());
+        if ((rc = upload(P.wslayers, &c->d_wslayers)) != DF_OK || (rc = upload(P.wsstages, &c->d_wsstages)) != DF_OK ||
+            (rc = upload(P.wsblob, &c->d_wsblob)) != DF_OK || (rc = upload(wssched, &c->d_wssched)) != DF_OK ||
+            (rc = upload(P.wstables, &c->d_wstables)) != DF_OK) {
+            std::string m = last_error();
+            df_chain_destroy(c);
+            return set_err(rc, m);
+        }
+    }
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->d_bounds), sizeof(float) * (2 * P.n + 4));
     if (e != hipSuccess) {
         df_chain_destroy(c);
@@ -207,6 +225,20 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
         if (e != hipSuccess) {
             df_chain_destroy(c);
             return hip_err(e, "hipFuncSetAttribute(wide)");
+        }
+        if (P.wsplit) {
+            c->wstab_bytes = ((int)P.wstables.size() * 4 + 15) / 16 * 16;
+            c->wslds = (size_t)df::kWideBufs * df::kWideSplitStageBytes + c->wstab_bytes +
+                       (size_t)df::kWideWaves * 16 * df::kWideT * P.stride * 4;
+            if (c->wslds > 160 * 1024) {
+                df_chain_destroy(c);
+                return set_err(DF_ERR_UNSUPPORTED, "wide SPLIT kernel needs more than 160 KiB of LDS");
+            }
+            e = df::set_wide_lds_limit(c->wslds, true);
+            if (e != hipSuccess) {
+                df_chain_destroy(c);
+                return hip_err(e, "hipFuncSetAttribute(wide split)");
+            }
         }
     }
     if (P.split) {
@@ -253,9 +285,9 @@ static void fill_info(const df::Plan& P, df_chain_info* out) {
     out->n_params = P.n_params;
     out->flops_per_sample = P.flops_per_sample;
     out->weight_bytes = (int64_t)P.blob.size();
-    out->kernel = P.wide ? 5 : P.split ? 4 : uniform_variant(P);
+    out->kernel = P.wide ? (P.wsplit ? 6 : 5) : P.split ? 4 : uniform_variant(P);
     out->reserved = 0;
-    out->split_flops_per_sample = P.split ? P.split_flops_per_sample : 0.0;
+    out->split_flops_per_sample = (P.split || P.wsplit) ? P.split_flops_per_sample : 0.0;
 }
 
 int df_chain_get_info(const df_chain* c, df_chain_info* out) {
@@ -295,7 +327,8 @@ int df_chain_set_weights(df_chain* c, const df_chain_desc* desc) {
                       P.ulayers.size() == Q.ulayers.size() && P.wlayers.size() == Q.wlayers.size() &&
                       same_bytes(P.wstages, Q.wstages) && P.wblob.size() == Q.wblob.size() &&
                       P.wbias.size() == Q.wbias.size() && same_bytes(P.pack_dst, Q.pack_dst) &&
-                      P.split == Q.split && same_bytes(P.sstages, Q.sstages) && P.sblob.size() == Q.sblob.size();
+                      P.split == Q.split && same_bytes(P.sstages, Q.sstages) && P.sblob.size() == Q.sblob.size() &&
+                      P.wsplit == Q.wsplit && same_bytes(P.wsstages, Q.wsstages) && P.wsblob.size() == Q.wsblob.size();
     if (!same) return set_err(DF_ERR_SHAPE, "df_chain_set_weights: the descriptor's structure differs from the chain's");
     for (size_t i = 0; i < P.layers.size(); ++i)
         if (P.layers[i].kind != Q.layers[i].kind || P.layers[i].n_af != Q.layers[i].n_af)
@@ -312,6 +345,8 @@ int df_chain_set_weights(df_chain* c, const df_chain_desc* desc) {
         return rc;
     if (P.split && ((rc = refresh(P.sulayers, c->d_sulayers)) != DF_OK || (rc = refresh(P.sblob, c->d_sblob)) != DF_OK))
         return rc;
+    if (P.wsplit && ((rc = refresh(P.wslayers, c->d_wslayers)) != DF_OK || (rc = refresh(P.wsblob, c->d_wsblob)) != DF_OK))
+        return rc;
     c->plan.layers = P.layers;
     c->plan.ulayers = P.ulayers;
     c->plan.wlayers = P.wlayers;
@@ -321,6 +356,8 @@ int df_chain_set_weights(df_chain* c, const df_chain_desc* desc) {
     c->plan.wbias.swap(P.wbias);
     c->plan.sulayers = P.sulayers;
     c->plan.sblob.swap(P.sblob);
+    c->plan.wslayers = P.wslayers;
+    c->plan.wsblob.swap(P.wsblob);
     c->plan.trainables.swap(P.trainables);
     return DF_OK;
 }
@@ -376,7 +413,7 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
         if (dbg[0] == '1') {
             std::fprintf(stderr, "[df] mode %d batch %lld kernel %s tiles %d (max %d) occupancy:", mode,
                          (long long)batch,
-                         wide ? "wide" : !P.uniform ? "generic" : split ? "uniform-fast-split" : P.fast ? "uniform-fast" : "uniform",
+                         wide ? (use_wsplit(c) ? "wide-split" : "wide") : !P.uniform ? "generic" : split ? "uniform-fast-split" : P.fast ? "uniform-fast" : "uniform",
                          tiles, split ? P.stiles : P.tiles);
             for (int t = 1; t <= (split ? P.stiles : P.tiles); ++t)
                 std::fprintf(stderr, " t%d=%d", t, split ? c->socc[mode][t] : c->occ[mode][t]);
@@ -445,7 +482,21 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
         a.n_sched_bwd = (int)P.wsched_bwd.size();
         a.wlayers = static_cast<const df::WLayer*>(c->d_wlayers);
         a.wbias = static_cast<const float*>(c->d_wbias);
-        e = df::launch_wide(mode, a, (unsigned)grid, c->wide_lds, st);
+        if (use_wsplit(c)) {
+            a.blob = static_cast<const uint8_t*>(c->d_wsblob);
+            a.stages = static_cast<const df::DevStage*>(c->d_wsstages);
+            a.sched_fwd = static_cast<const int32_t*>(c->d_wssched);
+            a.sched_bwd = a.sched_fwd + P.wssched_fwd.size();
+            a.n_sched_fwd = (int)P.wssched_fwd.size();
+            a.n_sched_bwd = (int)P.wssched_bwd.size();
+            a.wlayers = static_cast<const df::WLayer*>(c->d_wslayers);
+            a.tables = static_cast<const int32_t*>(c->d_wstables);
+            a.tab_ints = (int)P.wstables.size();
+            a.tab_bytes = c->wstab_bytes;
+            e = df::launch_wide(mode, a, (unsigned)grid, c->wslds, st, true);
+        } else {
+            e = df::launch_wide(mode, a, (unsigned)grid, c->wide_lds, st);
+        }
     } else if (split) {
         a.blob = static_cast<const uint8_t*>(c->d_sblob);
         a.stages = static_cast<const df::DevStage*>(c->d_sstages);

@@ -52,10 +52,19 @@ struct df_chain {
     int sn_stage_bufs = 1;
     size_t slds = 0;
     int socc[4][df::kMaxTilesPerWave + 1] = {};
+    // SPLIT variant of the wide kernel (plan.wsplit)
+    void* d_wslayers = nullptr;
+    void* d_wsstages = nullptr;
+    void* d_wsblob = nullptr;
+    void* d_wssched = nullptr;
+    void* d_wstables = nullptr;
+    int wstab_bytes = 0;
+    size_t wslds = 0;
 };
 
 // SPLIT launches unless DF_F32_EXACT=1 (read per launch: an A/B knob for tests and benches)
 bool use_split(const df_chain* c);
+bool use_wsplit(const df_chain* c);
 
 namespace df {
 namespace api {

@@ -75,7 +75,8 @@ hipError_t kernel_occupancy(int ht, int mode, bool outv, int uniform, size_t lds
 hipError_t launch_reduce_partials(const double* part, int64_t n, double* out, hipStream_t st);
 
 // Wide-net kernel (df_wide.hip): 4-wave workgroups of kWideWaves*16*kWideT samples.
-hipError_t launch_wide(int mode, const ChainArgs& a, unsigned grid, size_t lds, hipStream_t st);
-hipError_t set_wide_lds_limit(size_t lds);
+// split: the SPLIT variant (bf16x3 products; a.blob / stages / schedules / wlayers / tables are the split ones)
+hipError_t launch_wide(int mode, const ChainArgs& a, unsigned grid, size_t lds, hipStream_t st, bool split = false);
+hipError_t set_wide_lds_limit(size_t lds, bool split = false);
 
 }  // namespace df

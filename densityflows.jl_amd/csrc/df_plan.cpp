@@ -434,6 +434,92 @@ void build_wide(const df_chain_desc* desc, Plan& P) {
     P.wide = 1;
 }
 
+// SPLIT packing of a wide plan (see Plan::wsplit): per net, ceil(in/32) first-Dense
+// stages, 8 hidden stages, one output stage, each chunk [m][plane][lane][8 bf16]
+// with lane (g, i) holding W[16m + i, k(e)], e < 8:
+//   first Dense  k = 32c + 8g + e (features through the layer's split table)
+//   hidden/out   k = 32c + 16(e>>2) + 4g + (e&3) (accumulator tiles 2c, 2c+1)
+void build_wide_split(const df_chain_desc* desc, Plan& P) {
+    P.wsplit = 0;
+    if (!P.wide) return;
+    if (const char* e = std::getenv("DF_F32_EXACT"))
+        if (e[0] == '1') return;
+    P.wstables = P.tables;
+    P.wslayers = P.wlayers;
+    const int zero_slot = P.n + P.d;
+    for (int li = 0; li < desc->n_layers; ++li) {
+        const df_layer_desc& L = desc->layers[li];
+        if (L.kind == DF_LAYER_NORM) continue;
+        const DevLayer& DL = P.layers[li];
+        WLayer& W = P.wslayers[li];
+        const int nc0 = (L.n_nn + 31) / 32;
+        W.pad0 = (int32_t)P.wstables.size();
+        for (int k = 0; k < 32 * nc0; ++k) P.wstables.push_back(k < L.n_nn ? L.axis_nn[k] - 1 : zero_slot);
+        auto pack = [&](const df_dense_desc* net, int d0, WNet& N) {
+            N.stage0 = (int)P.wsstages.size();
+            N.nst0 = nc0;
+            auto new_stage = [&](int bytes) -> int64_t {
+                DevStage st{};
+                st.src_off = (int64_t)P.wsblob.size();
+                st.bytes = bytes;
+                P.wsstages.push_back(st);
+                P.wsblob.resize(P.wsblob.size() + bytes, 0);
+                return st.src_off;
+            };
+            // chunk [m < mt][plane][lane][8] of m-tiles m0 + m at byte `base` of the blob, k(c, g, e) as above
+            auto chunk = [&](int64_t base, int dense, int c, int mt, bool first, int m0 = 0) {
+                const df_dense_desc& D = net[dense];
+                for (int m = 0; m < mt; ++m)
+                    for (int p = 0; p < 3; ++p)
+                        for (int lane = 0; lane < 64; ++lane)
+                            for (int e = 0; e < 8; ++e) {
+                                const int g = lane >> 4, row = 16 * (m0 + m) + (lane & 15);
+                                const int k = first ? 32 * c + 8 * g + e : 32 * c + 16 * (e >> 2) + 4 * g + (e & 3);
+                                const int64_t at = base + (((int64_t)m * 3 + p) * 64 + lane) * 16 + 2 * e;
+                                uint16_t h = 0;
+                                if (row < D.out_dim && k < D.in_dim) {
+                                    h = bf16_split_plane(D.W[(size_t)row + (size_t)D.out_dim * k], p);
+                                    P.wspack_dst.push_back((int32_t)at);
+                                    P.wspack_src.push_back((P.denses[d0 + dense].w_off + row + D.out_dim * k) * 4 + p);
+                                }
+                                std::memcpy(&P.wsblob[at], &h, 2);
+                            }
+            };
+            for (int c = 0; c < nc0; ++c) chunk(new_stage(kWideSplitStageBytes), 0, c, 16, true);
+            for (int c = 0; c < 8; ++c) chunk(new_stage(kWideSplitStageBytes), 1, c, 16, false);
+            const int64_t ob = new_stage(8 * N.mto * 3 * 1024);
+            for (int c = 0; c < 8; ++c) chunk(ob + (int64_t)c * N.mto * 3 * 1024, 2, c, N.mto, false);
+            P.split_flops_per_sample += 2.0 * ((double)net[0].in_dim * net[0].out_dim +
+                                               (double)net[1].in_dim * net[1].out_dim +
+                                               (double)net[2].in_dim * net[2].out_dim);
+        };
+        if (L.kind == DF_LAYER_RNVP) pack(L.s_net, DL.s_dense0, W.s);
+        pack(L.t_net, DL.t_dense0, W.t);
+    }
+    auto sched = [&](bool fwd) {
+        std::vector<int32_t> out;
+        auto net = [&](const WNet& N) {
+            for (int s = 0; s < N.nst0 + 9; ++s) out.push_back(N.stage0 + s);
+        };
+        for (int it = 0; it < P.n_layers; ++it) {
+            const WLayer& L = P.wslayers[fwd ? it : P.n_layers - 1 - it];
+            if (L.kind == DF_LAYER_NORM) continue;
+            if (fwd) {
+                if (L.kind == DF_LAYER_RNVP) net(L.s);
+                net(L.t);
+            } else {
+                net(L.t);
+                if (L.kind == DF_LAYER_RNVP) net(L.s);
+            }
+        }
+        return out;
+    };
+    P.wssched_fwd = sched(true);
+    P.wssched_bwd = sched(false);
+    P.wsblob.resize(P.wsblob.size() + 16, 0);
+    P.wsplit = 1;
+}
+
 }  // namespace
 
 size_t plan_lds_bytes(const Plan& p) {
@@ -988,6 +1074,7 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
         P.blob.resize(round_up((int)P.blob.size(), 16) + 16, 0);
         build_split(desc, P, fold);
         build_wide(desc, P);
+        build_wide_split(desc, P);
         *out = std::move(P);
         return DF_OK;
     } catch (const Fail& f) {

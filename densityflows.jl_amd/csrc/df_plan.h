@@ -120,6 +120,7 @@ constexpr int kWideStageBytes = 32 * 1024;
 constexpr int kWideBufs = DF_WIDE_NB;   // LDS stage ring: the DMA runs kWideBufs − 1 stages ahead
 constexpr int kWideWaves = 4;     // one wave per SIMD (512 registers each)
 constexpr int kWideT = 2;         // 16-sample tiles per wave held in registers (3 spills)
+constexpr int kWideSplitStageBytes = 48 * 1024;  // SPLIT: one 32-input chunk of 16 m-tiles × 3 planes
 
 struct WNet {
     int32_t stage0;   // first stage id (wide blob)
@@ -228,6 +229,17 @@ struct Plan {
     std::vector<int32_t> ssched_fwd, ssched_bwd;
     // sblob byte offset ← trainables index·4 + plane (plane 3: the f32 value itself)
     std::vector<int32_t> spack_dst, spack_src;
+    // SPLIT variant of the wide kernel (plan.wide): first, hidden and output Dense
+    // as bf16x3 products; stages of up to kWideSplitStageBytes ([m][plane][lane][8]
+    // per 32-input chunk), WLayer::pad0 = the layer's split feature table (32·nst0
+    // slots); biases stay in wbias.
+    int wsplit = 0;
+    std::vector<WLayer> wslayers;
+    std::vector<DevStage> wsstages;
+    std::vector<uint8_t> wsblob;
+    std::vector<int32_t> wssched_fwd, wssched_bwd;
+    std::vector<int32_t> wspack_dst, wspack_src;  // wsblob byte offset ← trainables index·4 + plane
+    std::vector<int32_t> wstables;                // tables + the split feature tables (wide SPLIT launches)
     double flops_per_sample = 0.0;
     double split_flops_per_sample = 0.0;  // the part of flops_per_sample the SPLIT kernel runs on bf16 MFMA
 };

@@ -136,9 +136,11 @@ struct df_train {
     void* d_wsrc = nullptr;
     void* d_wbdst = nullptr;
     void* d_wbsrc = nullptr;
-    // repack map of the chain's SPLIT blob (plan.split)
+    // repack maps of the chain's SPLIT blobs (plan.split, plan.wsplit)
     void* d_sdst = nullptr;
     void* d_ssrc = nullptr;
+    void* d_wsdst = nullptr;
+    void* d_wssrc = nullptr;
 };
 
 namespace {
@@ -158,7 +160,8 @@ void free_all(df_train* t) {
     void* ptrs[] = {t->d_params, t->d_m,    t->d_v,    t->d_grad, t->d_partial, t->d_tblob, t->d_pdst,
                     t->d_psrc,   t->d_tdst, t->d_tsrc, t->d_snap, t->d_zbar,    t->d_ebuf,  t->d_lpsum,
                     t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_lyp[0], t->d_lyp[1], t->d_lbp[0], t->d_lbp[1], t->d_lx, t->d_hsave,
-                    t->d_wdst,   t->d_wsrc, t->d_wbdst, t->d_wbsrc, t->d_sdst, t->d_ssrc};
+                    t->d_wdst,   t->d_wsrc, t->d_wbdst, t->d_wbsrc, t->d_sdst, t->d_ssrc,
+                    t->d_wsdst, t->d_wssrc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (float* p : t->d_lh)
@@ -445,6 +448,10 @@ int repack(df_train* t, hipStream_t st) {
     if (e == hipSuccess && P.split)
         e = launch_repack_split(static_cast<uint8_t*>(c->d_sblob), static_cast<const int32_t*>(t->d_sdst),
                                 static_cast<const int32_t*>(t->d_ssrc), (int64_t)P.spack_dst.size(), t->d_params, st);
+    if (e == hipSuccess && P.wsplit)
+        e = launch_repack_split(static_cast<uint8_t*>(c->d_wsblob), static_cast<const int32_t*>(t->d_wsdst),
+                                static_cast<const int32_t*>(t->d_wssrc), (int64_t)P.wspack_dst.size(), t->d_params,
+                                st);
     if (e == hipSuccess && !t->ldst.empty())
         e = launch_repack(static_cast<float*>(t->d_lblob), static_cast<const int32_t*>(t->d_ldst),
                           static_cast<const int32_t*>(t->d_lsrc), (int64_t)t->ldst.size(), t->d_params, st);
@@ -822,7 +829,8 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
         (rc = upload(P.wbias_src, &t->d_wbsrc)) != DF_OK ||
         (rc = upload(P.pack_src, &t->d_psrc)) != DF_OK || (rc = upload(t->tdst, &t->d_tdst)) != DF_OK ||
         (rc = upload(t->tsrc, &t->d_tsrc)) != DF_OK || (rc = upload(P.spack_dst, &t->d_sdst)) != DF_OK ||
-        (rc = upload(P.spack_src, &t->d_ssrc)) != DF_OK) {
+        (rc = upload(P.spack_src, &t->d_ssrc)) != DF_OK || (rc = upload(P.wspack_dst, &t->d_wsdst)) != DF_OK ||
+        (rc = upload(P.wspack_src, &t->d_wssrc)) != DF_OK) {
         std::string m = last_error();
         df_train_destroy(t);
         return set_err(rc, m);

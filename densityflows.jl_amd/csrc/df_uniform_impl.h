@@ -423,15 +423,20 @@ __device__ __forceinline__ void dense_first_split(const uint8_t* buf, const UNet
 
 // Hidden H×H Dense: k-chunk c of 32 inputs = accumulator tiles 2c, 2c+1 (lane
 // (g, j): rows 32c + 16(e>>2) + 4g + (e&3) of sample j), split on the fly.
+// The accumulators start from the bias (b + W·x: the sum's rounding order differs
+// from Flux's W*x .+ b by one f32 rounding, like any other summation order).
 template <int HT, int TT>
 __device__ __forceinline__ void dense_hidden_split(const uint8_t* wb, const f32x4 (&in)[TT][HT],
                                                    f32x4 (&out)[TT][HT]) {
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const uint8_t* bb = wb + (HT / 2) * HT * 3072;
     wb += lane * 16;
 #pragma unroll
-    for (int t = 0; t < TT; ++t)
+    for (int m = 0; m < HT; ++m) {
+        const f32x4 b = lds4(bb + ((16 * m + 4 * g) << 2));
 #pragma unroll
-        for (int m = 0; m < HT; ++m) out[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < TT; ++t) out[t][m] = b;
+    }
 #pragma unroll
     for (int c = 0; c < HT / 2; ++c) {
         bf16x8 x[TT][3];
@@ -477,7 +482,7 @@ __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, con
         dense_first_split<HT, TT>(buf, N, xin, A);
         bias_act<HT, TT, true>(buf, DF_ACT_RELU, A, false);
         dense_hidden_split<HT, TT>(buf + N.off_h, A, B);
-        bias_act<HT, TT, true>(buf + N.off_h + (HT / 2) * HT * 3072, DF_ACT_RELU, B);
+        bias_act<HT, TT, true>(buf, DF_ACT_RELU, B, false);
         tail<HT, TT, OUTV, RELU, PH, NO>(buf, N, L, tab, state, ro, sum, B);
         return;
     }

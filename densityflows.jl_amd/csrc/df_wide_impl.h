@@ -60,15 +60,17 @@ struct WStager {
     int n;
     int idx;
     int cur;
+    int bytes;  // ring slot size: kWideStageBytes, or kWideSplitStageBytes (SPLIT)
     __device__ __forceinline__ uint8_t* buf() const { return slot(idx); }
-    __device__ __forceinline__ uint8_t* slot(int i) const { return base + (i % kWideBufs) * kWideStageBytes; }
+    __device__ __forceinline__ uint8_t* slot(int i) const { return base + (i % kWideBufs) * bytes; }
 };
 
 // DMA instructions wave w issues for a stage of `bytes` (1 KiB per instruction,
 // chunks dealt round-robin over the waves).
+template <int NW>
 __device__ __forceinline__ int dma_ops(int bytes, int wave) {
     const int nchunk = bytes >> 10;
-    return nchunk > wave ? (nchunk - wave + kWideWaves - 1) / kWideWaves : 0;
+    return nchunk > wave ? (nchunk - wave + NW - 1) / NW : 0;
 }
 
 // s_waitcnt vmcnt(k) with k a run-time value (the count must be an immediate).
@@ -86,12 +88,13 @@ __device__ __forceinline__ void wait_vmcnt(int k) {
     }
 }
 
+template <int NW>
 __device__ __forceinline__ void dma(const ChainArgs& a, int s, uint8_t* dst) {
     const DevStage& st = cref(a.stages + s);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint8_t* src = a.blob + st.src_off;
     const int nchunk = st.bytes >> 10;
-    for (int c = wave; c < nchunk; c += kWideWaves)
+    for (int c = wave; c < nchunk; c += NW)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (c << 10) + lane * 16),
                                          (__attribute__((address_space(3))) void*)(dst + (c << 10)), 16, 0, 0);
 }
@@ -101,6 +104,7 @@ __device__ __forceinline__ void dma(const ChainArgs& a, int s, uint8_t* dst) {
 // Vector-memory loads return in order, so waiting until at most the newer
 // in-flight stages' DMA instructions of this wave are outstanding means this
 // wave's part of stage s has landed; the barrier then covers every wave's part.
+template <int NW = kWideWaves>
 __device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
     if (s == sg.cur) return;
     const int nidx = sg.idx + 1;
@@ -108,7 +112,7 @@ __device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
         const int wave = threadIdx.x >> 6;
         int newer = 0;
         for (int q = 1; q < kWideBufs - 1; ++q)
-            if (nidx + q < sg.n) newer += dma_ops(cref(a.stages + cref(sg.sched + nidx + q)).bytes, wave);
+            if (nidx + q < sg.n) newer += dma_ops<NW>(cref(a.stages + cref(sg.sched + nidx + q)).bytes, wave);
         wait_vmcnt(newer);
     } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -125,12 +129,12 @@ __device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
         const DevStage st = a.stages[s];
         const f32x4* src = reinterpret_cast<const f32x4*>(a.blob + st.src_off);
         f32x4* dst = reinterpret_cast<f32x4*>(sg.buf());
-        for (int i = threadIdx.x; i < (st.bytes >> 4); i += kThreads) dst[i] = src[i];
+        for (int i = threadIdx.x; i < (st.bytes >> 4); i += NW * 64) dst[i] = src[i];
         __syncthreads();
         sg.n = 0;
         return;
     }
-    if (nidx + kWideBufs - 1 < sg.n) dma(a, cref(sg.sched + nidx + kWideBufs - 1), sg.slot(nidx + kWideBufs - 1));
+    if (nidx + kWideBufs - 1 < sg.n) dma<NW>(a, cref(sg.sched + nidx + kWideBufs - 1), sg.slot(nidx + kWideBufs - 1));
 }
 
 // h = σ.(acc .+ b)  (b: 256 floats in global memory, L2-resident)
@@ -292,16 +296,192 @@ __device__ __forceinline__ void eval_net(const ChainArgs& a, const WNet& N, cons
     }
 }
 
+// ---- SPLIT variant: every Dense as bf16x3 products on bf16 MFMA (df_uniform_impl.h) ----
+using uni::bf16x8;
+using uni::mfma_bf;
+using uni::split8;
+#ifndef DF_WSPLIT_WAVES
+#define DF_WSPLIT_WAVES 4
+#endif
+constexpr int kSplitWaves = DF_WSPLIT_WAVES;         // 4: one wave per SIMD, 2 tiles; 8: two, 1 tile
+constexpr int kSplitT = 8 / DF_WSPLIT_WAVES;        // 128 samples per workgroup either way
+
+// acc += W·x over one 32-input chunk for m-tiles [0, MT): planes [m][p][lane][8] at
+// buf (lane offset applied), activation planes x[t][p]; the next m-tile's planes
+// are read while this one's 6·TT MFMAs run.
+//   HILO: the leading product w0·x0 goes to hi, the five correction products
+//   (small terms first) to lo.  Inside one MFMA a sum of products is truncated
+//   toward zero (tools/probe/mfma_round.hip: C + ONE product rounds to nearest
+//   even, several do not), so a running total fed back as the C operand six times
+//   per chunk took a biased rounding each time: at config 4 (eight chunks) that
+//   doubled the 99th-percentile error against the exact-f32 kernel.  With hi/lo
+//   the total takes one per chunk and lo's are relative to the small terms.  hi
+//   and lo are touched only by MFMAs (AGPR-resident); the caller adds them once.
+//   !HILO (the one- or two-chunk first Dense): all six products onto hi.
+template <int TT, int MT, bool HILO, int MA>
+__device__ __forceinline__ void split_chunk(const uint8_t* buf, const bf16x8 (&x)[TT][3], f32x4 (&hi)[TT][MA],
+                                            f32x4 (&lo)[TT][MA]) {
+    bf16x8 w[2][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) w[0][p] = *reinterpret_cast<const bf16x8*>(buf + p * 1024);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int cb = m & 1;
+        if (m + 1 < MT) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) w[cb ^ 1][p] = *reinterpret_cast<const bf16x8*>(buf + (m + 1) * 3072 + p * 1024);
+        }
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            f32x4 v = HILO ? lo[t][m] : hi[t][m];
+            v = mfma_bf(w[cb][2], x[t][0], v);
+            v = mfma_bf(w[cb][1], x[t][1], v);
+            v = mfma_bf(w[cb][0], x[t][2], v);
+            v = mfma_bf(w[cb][1], x[t][0], v);
+            v = mfma_bf(w[cb][0], x[t][1], v);
+            if (HILO) {
+                lo[t][m] = v;
+                hi[t][m] = mfma_bf(w[cb][0], x[t][0], hi[t][m]);
+            } else {
+                hi[t][m] = mfma_bf(w[cb][0], x[t][0], v);
+            }
+        }
+        asm volatile("" ::: "memory");  // fragment reads stay one m-tile ahead (no hoisting)
+    }
+}
+
+// Planes of accumulator tiles 2c, 2c+1 (inputs 32c + 16(e>>2) + 4g + (e&3)).
+template <int TT>
+__device__ __forceinline__ void split_tiles(const f32x4 (&h)[TT][16], int c, bf16x8 (&x)[TT][3]) {
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+        const float v[8] = {h[t][2 * c][0],     h[t][2 * c][1],     h[t][2 * c][2],     h[t][2 * c][3],
+                            h[t][2 * c + 1][0], h[t][2 * c + 1][1], h[t][2 * c + 1][2], h[t][2 * c + 1][3]};
+        split8(v, x[t][0], x[t][1], x[t][2]);
+    }
+}
+
+// eval_net on the SPLIT stages (layout: build_wide_split): accumulators start from
+// the bias (b + W·x), relu after.
+//   first Dense  ceil(in/32) stages [m < 16][p][lane][8], lane group g carries
+//                features 32c + 8g + e
+//   hidden Dense 8 stages [m < 16][p][lane][8], one 32-input chunk each (hi/lo)
+//   output Dense one stage [c < 8][m < mto][p][lane][8] (hi/lo)
+template <int TT>
+__device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N, const int32_t* sfeat,
+                                               const float* state, const int (&ro)[TT], WStager& sg,
+                                               f32x4 (&out)[TT][2], float* hs, const int64_t (&gs)[TT]) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    f32x4 h[TT][16], acc[TT][16], lo[TT][16];
+
+    // ---- first Dense ----
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const f32x4 b = bias4(a.wbias + N.b0, m);
+#pragma unroll
+        for (int t = 0; t < TT; ++t) acc[t][m] = b;
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        if (c < N.nst0) {
+            ensure<kSplitWaves>(N.stage0 + c, sg, a);
+            bf16x8 x[TT][3];
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = state[ro[t] + sfeat[32 * c + 8 * g + e]];
+                split8(v, x[t][0], x[t][1], x[t][2]);
+            }
+            split_chunk<TT, 16, false>(sg.buf() + lane * 16, x, acc, acc);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[t][m][r] = uni::relu_fast(acc[t][m][r]);
+
+    // ---- hidden Dense 256×256 ----
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const f32x4 b = bias4(a.wbias + N.b1, m);
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            acc[t][m] = b;
+            lo[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        ensure<kSplitWaves>(N.stage0 + N.nst0 + c, sg, a);
+        if (hs && c == 0) {  // training: keep H0 (as in eval_net)
+#pragma unroll
+            for (int t = 0; t < TT; ++t)
+                if (gs[t] >= 0)
+#pragma unroll
+                    for (int m = 0; m < 16; ++m)
+                        __builtin_nontemporal_store(h[t][m], reinterpret_cast<f32x4*>(hs + gs[t] * a.hsave_w + 16 * m + 4 * g));
+        }
+        bf16x8 x[TT][3];
+        split_tiles<TT>(h, c, x);
+        split_chunk<TT, 16, true>(sg.buf() + lane * 16, x, acc, lo);
+    }
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const f32x4 v = acc[t][m] + lo[t][m];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[t][m][r] = uni::relu_fast(v[r]);
+        }
+
+    // ---- output Dense (<= 32 outputs) ----
+    ensure<kSplitWaves>(N.stage0 + N.nst0 + 8, sg, a);
+    if (hs) {  // training: keep H1
+        float* hs1 = hs + a.batch * a.hsave_w;
+#pragma unroll
+        for (int t = 0; t < TT; ++t)
+            if (gs[t] >= 0)
+#pragma unroll
+                for (int m = 0; m < 16; ++m)
+                    __builtin_nontemporal_store(h[t][m], reinterpret_cast<f32x4*>(hs1 + gs[t] * a.hsave_w + 16 * m + 4 * g));
+    }
+    const uint8_t* buf = sg.buf() + lane * 16;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const f32x4 b = m < N.mto ? bias4(a.wbias + N.bo, m) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            acc[t][m] = b;
+            lo[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        bf16x8 x[TT][3];
+        split_tiles<TT>(h, c, x);
+        if (N.mto == 2) split_chunk<TT, 2, true>(buf + c * 2 * 3072, x, acc, lo);
+        else split_chunk<TT, 1, true>(buf + c * 3072, x, acc, lo);
+    }
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+        out[t][0] = acc[t][0] + lo[t][0];
+        out[t][1] = acc[t][1] + lo[t][1];
+    }
+}
+
 // Coupling phase on the transformed dims (row o = 16m + 4g + r of out ↔ axis_af[o]);
 // sum[t] = Σ_o s_o for the s phases.
-template <int PH>
-__device__ __forceinline__ void couple(const f32x4 (&out)[T][2], const WLayer& L, const int32_t* tab, float* state,
-                                       const int (&ro)[T], float (&sum)[T]) {
+template <int PH, int TT = T>
+__device__ __forceinline__ void couple(const f32x4 (&out)[TT][2], const WLayer& L, const int32_t* tab, float* state,
+                                       const int (&ro)[TT], float (&sum)[TT]) {
     const int g = (threadIdx.x & 63) >> 4;
     constexpr bool SPH = (PH == impl::PH_S_FWD || PH == impl::PH_S_BWD);
     const int32_t* af = tab + L.af_tab;
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
+    for (int t = 0; t < TT; ++t) {
         float p = 0.f;
 #pragma unroll
         for (int m = 0; m < 2; ++m)
@@ -321,14 +501,18 @@ __device__ __forceinline__ void couple(const f32x4 (&out)[T][2], const WLayer& L
 
 }  // namespace wide
 
-template <int MODE>
-__global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
+template <int MODE, bool SPLIT = false>
+__global__ void __launch_bounds__(SPLIT ? wide::kSplitWaves * 64 : wide::kThreads, 1) wide_kernel(ChainArgs a) {
     using namespace wide;
     constexpr bool FWD = (MODE == MODE_FWD || MODE == MODE_FWD_INPLACE);
     constexpr bool WANT_LDJ = (MODE != MODE_FWD_INPLACE);
+    constexpr int SBYTES = SPLIT ? kWideSplitStageBytes : kWideStageBytes;
+    constexpr int NW = SPLIT ? kSplitWaves : kWideWaves;  // waves
+    constexpr int TT = SPLIT ? kSplitT : T;               // 16-sample tiles per wave
+    constexpr int NT = NW * 64;
 
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int stage_area = kWideBufs * kWideStageBytes;
+    const int stage_area = kWideBufs * SBYTES;
     int32_t* tab = reinterpret_cast<int32_t*>(smem + stage_area);
     float* state = reinterpret_cast<float*>(smem + stage_area + a.tab_bytes);
 
@@ -336,7 +520,7 @@ __global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
     const int lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, j = lane & 15;
     const int d = a.d, n = a.n, stride = a.stride, nd = n + d;
-    constexpr int S = kWideWaves * 16 * T;
+    constexpr int S = NW * 16 * TT;
     const int cA = nd + 1, cE = nd + 2;
     const int64_t s0 = (int64_t)blockIdx.x * S;
     const int nvalid = (int)((a.batch - s0) < S ? (a.batch - s0) : S);
@@ -347,14 +531,15 @@ __global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
     sg.n = FWD ? a.n_sched_fwd : a.n_sched_bwd;
     sg.idx = -1;
     sg.cur = -1;
-    for (int q = 0; q < kWideBufs - 1 && q < sg.n; ++q) dma(a, cref(sg.sched + q), sg.slot(q));
+    sg.bytes = SBYTES;
+    for (int q = 0; q < kWideBufs - 1 && q < sg.n; ++q) dma<NW>(a, cref(sg.sched + q), sg.slot(q));
 
-    for (int i = tid; i < a.tab_ints; i += kThreads) tab[i] = a.tables[i];
-    for (int i = tid; i < S * d; i += kThreads) {
+    for (int i = tid; i < a.tab_ints; i += NT) tab[i] = a.tables[i];
+    for (int i = tid; i < S * d; i += NT) {
         const int smp = i / d, c = i - smp * d;
         state[smp * stride + n + c] = (smp < nvalid) ? a.zin[(s0 + smp) * d + c] : 0.f;
     }
-    for (int i = tid; i < S * n; i += kThreads) {
+    for (int i = tid; i < S * n; i += NT) {
         const int smp = i / n, c = i - smp * n;
         float v = 0.f;
         if (smp < nvalid) {
@@ -366,15 +551,15 @@ __global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
         }
         state[smp * stride + c] = v;
     }
-    for (int i = tid; i < S; i += kThreads)
+    for (int i = tid; i < S; i += NT)
         for (int c = nd; c < stride; ++c) state[i * stride + c] = 0.f;
     __syncthreads();
 
-    int ro[T];
-    int64_t gs[T];
+    int ro[TT];
+    int64_t gs[TT];
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-        const int smp = (wave * T + t) * 16 + j;
+    for (int t = 0; t < TT; ++t) {
+        const int smp = (wave * TT + t) * 16 + j;
         ro[t] = smp * stride;
         gs[t] = smp < nvalid ? s0 + smp : -1;
     }
@@ -397,7 +582,7 @@ __global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
             const float* xmn = a.params + L.norm_off;
             const float* xmx = xmn + d;
 #pragma unroll
-            for (int t = 0; t < T; ++t) {
+            for (int t = 0; t < TT; ++t) {
                 for (int i = g; i < d; i += 4) {
                     const float lo = xmn[i], hi = xmx[i], xd = hi - lo;
                     float v = state[ro[t] + n + i];
@@ -418,12 +603,13 @@ __global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
             }
             auto run = [&](const WNet& N, auto ph_tag, float* hs, bool sphase, float sign) {
                 constexpr int PH = decltype(ph_tag)::value;
-                f32x4 out[T][2];
-                float sum[T];
-                eval_net(a, N, feat, state, ro, sg, out, hs, gs);
-                couple<PH>(out, L, tab, state, ro, sum);
+                f32x4 out[TT][2];
+                float sum[TT];
+                if constexpr (SPLIT) eval_net_split<TT>(a, N, tab + L.pad0, state, ro, sg, out, hs, gs);
+                else eval_net(a, N, feat, state, ro, sg, out, hs, gs);
+                couple<PH, TT>(out, L, tab, state, ro, sum);
 #pragma unroll
-                for (int t = 0; t < T; ++t) {
+                for (int t = 0; t < TT; ++t) {
                     if (sphase) ldj_update(ro[t], sign * sum[t], first_in_elem, last_in_elem);
                     else if (!rnvp) ldj_update(ro[t], 0.f, first_in_elem, last_in_elem);
                 }
@@ -444,7 +630,7 @@ __global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
         if (!FWD && a.snap) {  // training: keep every layer's output for the reverse sweep
             float* dst = a.snap + (int64_t)li * a.batch * d;
 #pragma unroll
-            for (int t = 0; t < T; ++t)
+            for (int t = 0; t < TT; ++t)
                 if (gs[t] >= 0)
                     for (int i = g; i < d; i += 4) dst[gs[t] * d + i] = state[ro[t] + n + i];
         }
@@ -455,7 +641,7 @@ __global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
         double part = 0.0;
         if (g == 0) {
 #pragma unroll
-            for (int t = 0; t < T; ++t) {
+            for (int t = 0; t < TT; ++t) {
                 float q = 0.f;
                 for (int i = 0; i < d; ++i) {
                     const float zz = state[ro[t] + n + i];
@@ -477,19 +663,19 @@ __global__ void __launch_bounds__(wide::kThreads, 1) wide_kernel(ChainArgs a) {
             __syncthreads();
             if (tid == 0) {
                 double s = 0.0;
-                for (int w = 0; w < kWideWaves; ++w) s += red[w];
+                for (int w = 0; w < NW; ++w) s += red[w];
                 a.partial[blockIdx.x] = s;
             }
         }
         if (!a.xout) return;
     }
     __syncthreads();
-    for (int i = tid; i < S * d; i += kThreads) {
+    for (int i = tid; i < S * d; i += NT) {
         const int smp = i / d, c = i - smp * d;
         if (smp < nvalid) a.xout[(s0 + smp) * d + c] = state[smp * stride + n + c];
     }
     if (WANT_LDJ && MODE != MODE_LOGPDF && a.ldj_out) {
-        for (int i = tid; i < nvalid; i += kThreads) a.ldj_out[s0 + i] = state[i * stride + cA];
+        for (int i = tid; i < nvalid; i += NT) a.ldj_out[s0 + i] = state[i * stride + cA];
     }
 }
 

@@ -129,10 +129,11 @@ typedef struct df_chain_info {
     int64_t weight_bytes;         /* packed device weight blob                */
     int32_t kernel;               /* chain-pass kernel: 0 generic, 1 specialised,
                                      2 specialised relu-only, 3 FAST, 4 FAST on
-                                     bf16x3 split stages (SPLIT), 5 wide       */
+                                     bf16x3 split stages (SPLIT), 5 wide,
+                                     6 wide SPLIT                              */
     int32_t reserved;
-    double split_flops_per_sample; /* part of flops_per_sample that kernel 4
-                                      runs as six bf16 products on MFMA      */
+    double split_flops_per_sample; /* part of flops_per_sample that kernels 4
+                                      and 6 run as six bf16 products on MFMA */
 } df_chain_info;
 
 int df_get_abi_version(void);

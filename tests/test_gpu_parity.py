@@ -477,7 +477,7 @@ def _kernel_of(chain):
     return chain.hip().info.kernel
 
 
-@pytest.mark.parametrize("name", ["cfg2", "fast_h32"])
+@pytest.mark.parametrize("name", ["cfg2", "fast_h32", "cfg4"])
 def test_split_variant_accuracy(cuda, name, monkeypatch):
     """The SPLIT variant (df_uniform_impl.h: first and hidden Dense on bf16 MFMA
     with both operands in three bf16 planes, six products, f32 accumulation) is an
@@ -486,11 +486,13 @@ def test_split_variant_accuracy(cuda, name, monkeypatch):
     median and the 99th percentile, for x and ldj in both directions; the worst
     (ill-conditioned) element within 2× the worst of the exact-f32 kernel and of
     Flux's op order in fp32."""
-    if name == "cfg2":
-        spec, g, meta = G.load("cfg2")
+    th = None
+    if name in ("cfg2", "cfg4"):
+        spec, g, meta = G.load(name)
         z, xin = g["z"], g["x_in"]
         xo, lo = g["x_fwd"], g["ldj_fwd"]
         zo, lbo = g["z_bwd"], g["ldj_bwd"]
+        th = g["theta"] if meta["n"] > 0 else None
     else:  # hidden 32 (HT = 2), 4 RNVP layers on d = 6
         rng = np.random.default_rng(7)
         ch = dfa.FlowChain.repeat(dfa.CouplingBlock, 2, 6, hidden_dim_s=32, hidden_dim_t=32, rng=rng)
@@ -500,15 +502,17 @@ def test_split_variant_accuracy(cuda, name, monkeypatch):
         xin = xo.astype(np.float32)
         zo, lbo = O.backward(spec, xin.astype(np.float64), np.zeros((0, 3000)), np.float64)
         z = z.astype(np.float32)
-    ref32 = list(O.forward(spec, z, np.zeros((0, z.shape[1]), np.float32), np.float32)) + \
-        list(O.backward(spec, xin, np.zeros((0, z.shape[1]), np.float32), np.float32))
+    th_np = th if th is not None else np.zeros((0, z.shape[1]), np.float32)
+    ref32 = list(O.forward(spec, z, th_np, np.float32)) + list(O.backward(spec, xin, th_np, np.float32))
+    wide = name == "cfg4"
     res = {}
     for exact in ("0", "1"):
         monkeypatch.setenv("DF_F32_EXACT", exact)
         chain = spec_to_element(spec)
-        assert _kernel_of(chain) == (3 if exact == "1" else 4)
-        x, lf = dfa.forward(chain, _t(z, cuda))
-        zb, lb = dfa.backward(chain, _t(xin, cuda))
+        assert _kernel_of(chain) == ((5 if wide else 3) if exact == "1" else (6 if wide else 4))
+        tth = _t(th, cuda) if th is not None else None
+        x, lf = dfa.forward(chain, _t(z, cuda), tth)
+        zb, lb = dfa.backward(chain, _t(xin, cuda), tth)
         res[exact] = [_np(v) for v in (x, lf, zb, lb)]
     print(f"strict relative error vs fp64 ({name}): quantity split(median, p99, max) | exact-f32(same)")
     for i, (key, truth) in enumerate((("x", xo), ("ldj", lo), ("z", zo), ("ldj_bwd", lbo))):
