@@ -38,6 +38,7 @@ constexpr int kLdwBN = 4;                //   × 4 column tiles (128 accumulator
 
 struct LDenseArgs {
     const uint8_t* wfrag;   // fragments [kq][m][lane][4] of A (M = 16·MT rows)
+    const uint8_t* sfrag;   // or (SPLIT, W1ᵀδ1 of hidden-256 nets) bf16x3 planes [c][m][p][lane][8], else nullptr
     const float* bias;      // 16·MT floats or nullptr
     int nkq, chunk_kq;
     int act;                // LEPI_ACT / LEPI_COUPLE: σ of this Dense
@@ -102,6 +103,8 @@ struct SweepJob {
 hipError_t launch_ldense(int mt, int in_kind, int epi, const LDenseArgs& a, unsigned grid, size_t lds,
                          hipStream_t st);
 hipError_t ldense_occupancy(int mt, int in_kind, int epi, size_t lds, int* blocks);
+// a SPLIT instance exists (LIN_BUF, 16 row tiles, δ epilogues)
+bool ldense_split_supported(int mt, int in_kind, int epi);
 hipError_t set_ldense_lds_limit(size_t lds);
 hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st);
 // Output Dense + coupling pullback → ȳ, then δ = (W_outᵀ ȳ) ⊙ σ'(H) in one pass over H

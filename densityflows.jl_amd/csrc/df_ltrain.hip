@@ -26,20 +26,32 @@ __device__ __forceinline__ float gather_feature(const LDenseArgs& a, int slot, i
 // One Dense over the whole batch: acc = A · in, A = packed W or Wᵀ (16·MT rows),
 // then the fused epilogue.  Persistent workgroups; each wave owns kLTiles
 // 16-sample tiles per round; A is streamed through two LDS chunk buffers.
-template <int MT, int IN, int EPI>
+// SPLIT (LIN_BUF, MT = 16): A = a.sfrag, bf16x3 planes [c][m][p][lane][8] of 32-input
+// chunks (lane (g, i): A[16m + i, 32c + 16(e>>2) + 4g + (e&3)]), the B rows split on
+// the fly (df_uniform_impl.h), six products per chunk on bf16 MFMA onto the f32
+// accumulators (gradients: the 1e-4 criterion of the training tests).
+template <int MT, int IN, int EPI, bool SPLIT = false>
 __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int T = kLTiles;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, j = lane & 15;
-    const int chunk_bytes = a.chunk_kq * MT * 1024;
-    const int nchunks = (a.nkq + a.chunk_kq - 1) / a.chunk_kq;
+    const int chunk_bytes = SPLIT ? MT * 3072 : a.chunk_kq * MT * 1024;
+    const int nchunks = SPLIT ? a.nkq / 2 : (a.nkq + a.chunk_kq - 1) / a.chunk_kq;
     const int64_t ntiles = (a.batch + 15) / 16;
     const int64_t per_round = (int64_t)gridDim.x * kWavesPerBlock * T;
     const int64_t rounds = (ntiles + per_round - 1) / per_round;
     const int64_t total = rounds * nchunks;
 
     auto dma = [&](int c, uint8_t* dst) {
+        if constexpr (SPLIT) {
+            const uint8_t* src = a.sfrag + (size_t)c * MT * 3072;
+            for (int q = wave; q < 3 * MT; q += kWavesPerBlock)
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (q << 10) + lane * 16),
+                                                 (__attribute__((address_space(3))) void*)(dst + (q << 10)), 16, 0,
+                                                 0);
+            return;
+        }
         const int kq0 = c * a.chunk_kq;
         const int kq1 = (kq0 + a.chunk_kq < a.nkq) ? kq0 + a.chunk_kq : a.nkq;
         const uint8_t* src = a.wfrag + (size_t)kq0 * MT * 1024;
@@ -50,7 +62,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
                                              0);
     };
     // after the chunk buffer(s): two full chunks, or the single (possibly short) one
-    uint8_t* w0t_lds = smem + (nchunks > 1 ? 2 * chunk_bytes : a.nkq * MT * 1024);
+    uint8_t* w0t_lds = smem + (nchunks > 1 ? 2 * chunk_bytes : SPLIT ? chunk_bytes : a.nkq * MT * 1024);
     if constexpr (EPI == LEPI_DACT_XBAR) {  // W0ᵀ fragments stay resident for the x̄ product
         const int n16 = a.w0t_mt * a.w0t_nkq * 64;
         const f32x4* src = reinterpret_cast<const f32x4*>(a.w0t);
@@ -109,6 +121,54 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
         constexpr int HR = MT < 8 ? MT : 8;  // σ' arguments in flight
         const int64_t s0h = valid[0] ? smp[0] : a.batch - 1;
         f32x4 h0[kDact ? HR : 1];
+        if constexpr (SPLIT && IN == LIN_BUF) {
+            f32x4 xn1[T];
+            load_x(1, xn1);
+            for (int c = 0; c < nchunks; ++c, ++i) {
+                const uint8_t* buf = smem;
+                if (nchunks > 1) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    if (i + 1 < total) dma((int)((i + 1) % nchunks), smem + (((i + 1) & 1) ? chunk_bytes : 0));
+                    buf = smem + ((i & 1) ? chunk_bytes : 0);
+                }
+                uni::bf16x8 xp[T][3];
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    const float v[8] = {xn[t][0],  xn[t][1],  xn[t][2],  xn[t][3],
+                                        xn1[t][0], xn1[t][1], xn1[t][2], xn1[t][3]};
+                    uni::split8(v, xp[t][0], xp[t][1], xp[t][2]);
+                }
+                if (c + 1 < nchunks) {
+                    load_x(2 * c + 2, xn);
+                    load_x(2 * c + 3, xn1);
+                }
+                if constexpr (kDact) {
+                    if (c + 1 == nchunks) {
+#pragma unroll
+                        for (int m = 0; m < HR; ++m)
+                            h0[m] = *reinterpret_cast<const f32x4*>(a.hprev + s0h * a.ld_h + 4 * g + 16 * m);
+                    }
+                }
+                const uint8_t* wb = buf + lane * 16;
+#pragma unroll
+                for (int m = 0; m < MT; ++m) {
+                    const uni::bf16x8 w0 = *reinterpret_cast<const uni::bf16x8*>(wb + m * 3072);
+                    const uni::bf16x8 w1 = *reinterpret_cast<const uni::bf16x8*>(wb + m * 3072 + 1024);
+                    const uni::bf16x8 w2 = *reinterpret_cast<const uni::bf16x8*>(wb + m * 3072 + 2048);
+#pragma unroll
+                    for (int t = 0; t < T; ++t) {  // small terms first
+                        f32x4 v = acc[t][m];
+                        v = uni::mfma_bf(w2, xp[t][0], v);
+                        v = uni::mfma_bf(w1, xp[t][1], v);
+                        v = uni::mfma_bf(w0, xp[t][2], v);
+                        v = uni::mfma_bf(w1, xp[t][0], v);
+                        v = uni::mfma_bf(w0, xp[t][1], v);
+                        acc[t][m] = uni::mfma_bf(w0, xp[t][0], v);
+                    }
+                }
+            }
+        } else
         for (int c = 0; c < nchunks; ++c, ++i) {
             const uint8_t* buf = smem;
             if (nchunks > 1) {
@@ -620,7 +680,13 @@ void* ldense_ptr_mt(int in_kind, int epi) {
     }
 }
 
-void* ldense_ptr(int mt, int in_kind, int epi) {
+void* ldense_ptr(int mt, int in_kind, int epi, bool split = false) {
+    if (split) {  // SPLIT instances: the W1ᵀδ1 products of hidden-256 conditioners
+        if (mt != 16 || in_kind != LIN_BUF) return nullptr;
+        if (epi == LEPI_DACT) return reinterpret_cast<void*>(&ldense_kernel<16, LIN_BUF, LEPI_DACT, true>);
+        if (epi == LEPI_DACT_XBAR) return reinterpret_cast<void*>(&ldense_kernel<16, LIN_BUF, LEPI_DACT_XBAR, true>);
+        return nullptr;
+    }
     switch (mt) {
         case 1: return ldense_ptr_mt<1>(in_kind, epi);
         case 2: return ldense_ptr_mt<2>(in_kind, epi);
@@ -633,9 +699,11 @@ void* ldense_ptr(int mt, int in_kind, int epi) {
 
 }  // namespace
 
+bool ldense_split_supported(int mt, int in_kind, int epi) { return ldense_ptr(mt, in_kind, epi, true) != nullptr; }
+
 hipError_t launch_ldense(int mt, int in_kind, int epi, const LDenseArgs& a, unsigned grid, size_t lds,
                          hipStream_t st) {
-    void* k = ldense_ptr(mt, in_kind, epi);
+    void* k = ldense_ptr(mt, in_kind, epi, a.sfrag != nullptr);
     if (!k) return hipErrorInvalidValue;
     void* args[] = {const_cast<LDenseArgs*>(&a)};
     return hipLaunchKernel(k, dim3(grid), dim3(kBlockThreads), args, lds, st);
@@ -655,6 +723,11 @@ hipError_t set_ldense_lds_limit(size_t lds) {
             if (e != hipSuccess) return e;
         }
         hipError_t e = hipFuncSetAttribute(ldense_ptr(mt, LIN_GATHER, LEPI_ACT),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    for (int epi : {LEPI_DACT, LEPI_DACT_XBAR}) {
+        hipError_t e = hipFuncSetAttribute(ldense_ptr(16, LIN_BUF, epi, true),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }

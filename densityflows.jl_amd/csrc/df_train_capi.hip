@@ -42,6 +42,7 @@ struct LOp {
     int chunk_kq = 1;        // k-quads per LDS chunk
     int64_t frag = 0;        // byte offset in the layer-wise blob
     int64_t bias = -1;       // float offset of the padded bias (forward only)
+    int64_t sfrag = -1;      // SPLIT planes [c][m][p][lane][8] in the split blob (Wᵀ of hidden-256 Denses)
 };
 
 struct LDense {
@@ -115,6 +116,11 @@ struct df_train {
     std::vector<LNet> lnets;
     std::vector<uint8_t> lblob;      // fragments (W and Wᵀ) then padded biases
     std::vector<int32_t> ldst, lsrc; // repack map (float index ← trainables index)
+    std::vector<uint8_t> lsblob;     // SPLIT planes of the layer-wise Wᵀ operands (LOp::sfrag)
+    std::vector<int32_t> lsdst, lssrc; // repack map (byte offset ← trainables index·4 + plane)
+    void* d_lsblob = nullptr;
+    void* d_lsdst = nullptr;
+    void* d_lssrc = nullptr;
     void* d_lblob = nullptr;
     void* d_ldst = nullptr;
     void* d_lsrc = nullptr;
@@ -161,7 +167,7 @@ void free_all(df_train* t) {
                     t->d_psrc,   t->d_tdst, t->d_tsrc, t->d_snap, t->d_zbar,    t->d_ebuf,  t->d_lpsum,
                     t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_lyp[0], t->d_lyp[1], t->d_lbp[0], t->d_lbp[1], t->d_lx, t->d_hsave,
                     t->d_wdst,   t->d_wsrc, t->d_wbdst, t->d_wbsrc, t->d_sdst, t->d_ssrc,
-                    t->d_wsdst, t->d_wssrc};
+                    t->d_wsdst, t->d_wssrc, t->d_lsblob, t->d_lsdst, t->d_lssrc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (float* p : t->d_lh)
@@ -199,6 +205,27 @@ LOp pack_lop(df_train* t, const Plan& P, const LDense& D, bool transposed) {
                     t->ldst.push_back((int32_t)(f0 + q));
                     t->lsrc.push_back((int32_t)src);
                 }
+    // SPLIT planes of a hidden-256 Wᵀ (the ldense_kernel SPLIT instances)
+    const char* ex = std::getenv("DF_F32_EXACT");
+    if (transposed && op.mt == 16 && op.nkq % 2 == 0 && !(ex && ex[0] == '1')) {
+        op.sfrag = (int64_t)t->lsblob.size();
+        t->lsblob.resize(t->lsblob.size() + (size_t)(op.nkq / 2) * op.mt * 3072, 0);
+        for (int c = 0; c < op.nkq / 2; ++c)
+            for (int m = 0; m < op.mt; ++m)
+                for (int p = 0; p < 3; ++p)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int e = 0; e < 8; ++e) {
+                            const int i = 16 * m + (lane & 15), g = lane >> 4;
+                            const int k = 32 * c + 16 * (e >> 2) + 4 * g + (e & 3);
+                            if (i >= rows || k >= kdim) continue;
+                            const int64_t src = D.w_off + k + (int64_t)D.out_dim * i;  // Wᵀ[i, k] = W[k, i]
+                            const int64_t at = op.sfrag + ((((int64_t)c * op.mt + m) * 3 + p) * 64 + lane) * 16 + 2 * e;
+                            const uint16_t h = bf16_split_plane(P.trainables[src], p);
+                            std::memcpy(&t->lsblob[at], &h, 2);
+                            t->lsdst.push_back((int32_t)at);
+                            t->lssrc.push_back((int32_t)(src * 4 + p));
+                        }
+    }
     return op;
 }
 
@@ -455,6 +482,9 @@ int repack(df_train* t, hipStream_t st) {
     if (e == hipSuccess && !t->ldst.empty())
         e = launch_repack(static_cast<float*>(t->d_lblob), static_cast<const int32_t*>(t->d_ldst),
                           static_cast<const int32_t*>(t->d_lsrc), (int64_t)t->ldst.size(), t->d_params, st);
+    if (e == hipSuccess && !t->lsdst.empty())
+        e = launch_repack_split(static_cast<uint8_t*>(t->d_lsblob), static_cast<const int32_t*>(t->d_lsdst),
+                                static_cast<const int32_t*>(t->d_lssrc), (int64_t)t->lsdst.size(), t->d_params, st);
     return e == hipSuccess ? DF_OK : hip_err(e, "repack kernel launch");
 }
 
@@ -470,14 +500,22 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
     const int W = t->lwidth;
     const uint8_t* lb = static_cast<const uint8_t*>(t->d_lblob);
     const float* lbf = static_cast<const float*>(t->d_lblob);
+    const uint8_t* lsb = static_cast<const uint8_t*>(t->d_lsblob);
+    const char* ex = std::getenv("DF_F32_EXACT");
+    const bool lsplit = !(ex && ex[0] == '1');
+    auto sfrag_of = [&](const LOp& op, int in_kind, int epi) -> const uint8_t* {
+        return (lsplit && op.sfrag >= 0 && ldense_split_supported(op.mt, in_kind, epi)) ? lsb + op.sfrag : nullptr;
+    };
     hipError_t e = hipSuccess;
     auto dense = [&](const LOp& op, int in_kind, int epi, LDenseArgs a) {
         a.wfrag = lb + op.frag;
         a.bias = (op.bias >= 0 && (epi == LEPI_ACT || epi == LEPI_COUPLE)) ? lbf + op.bias : nullptr;
         a.nkq = op.nkq;
         a.chunk_kq = op.chunk_kq;
+        a.sfrag = sfrag_of(op, in_kind, epi);
         const int nchunks = (op.nkq + op.chunk_kq - 1) / op.chunk_kq;
-        const size_t lds = (size_t)(nchunks > 1 ? 2 : 1) * std::min(op.nkq, op.chunk_kq) * op.mt * 1024;
+        const size_t lds = a.sfrag ? (size_t)(op.nkq / 2 > 1 ? 2 : 1) * op.mt * 3072
+                                   : (size_t)(nchunks > 1 ? 2 : 1) * std::min(op.nkq, op.chunk_kq) * op.mt * 1024;
         if (e == hipSuccess) e = launch_ldense(op.mt, in_kind, epi, a, dgrid, lds, st);
     };
     // Per net op: base arguments, and whether its backward front is the fused
@@ -643,8 +681,11 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
                     c2.w0t_nkq = N.dn[0].bwd.nkq;
                     const LOp& lo = N.dn[k].bwd;
                     const int nchunks = (lo.nkq + lo.chunk_kq - 1) / lo.chunk_kq;
-                    const size_t lds2 = (size_t)(nchunks > 1 ? 2 : 1) * std::min(lo.nkq, lo.chunk_kq) * lo.mt * 1024 +
-                                        (size_t)c2.w0t_mt * c2.w0t_nkq * 1024 + 64;  // + z̄ column table
+                    c2.sfrag = sfrag_of(lo, LIN_BUF, LEPI_DACT_XBAR);
+                    const size_t wbytes = c2.sfrag ? (size_t)(lo.nkq / 2 > 1 ? 2 : 1) * lo.mt * 3072
+                                                   : (size_t)(nchunks > 1 ? 2 : 1) * std::min(lo.nkq, lo.chunk_kq) *
+                                                         lo.mt * 1024;
+                    const size_t lds2 = wbytes + (size_t)c2.w0t_mt * c2.w0t_nkq * 1024 + 64;  // + z̄ column table
                     c2.wfrag = lb + lo.frag;
                     c2.nkq = lo.nkq;
                     c2.chunk_kq = lo.chunk_kq;
@@ -794,7 +835,7 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
     }
     t->grid = std::max(1, c->n_cu * occ);
     if (t->layerwise) {
-        e = set_ldense_lds_limit((size_t)2 * kLChunkBytes + 64 * 1024);
+        e = set_ldense_lds_limit(160 * 1024);
         if (e == hipSuccess) e = set_couple_bwd_lds_limit(64 * 1024);
         if (e == hipSuccess) e = set_sweep_lds_limit(std::max<size_t>(ldw_lds_bytes(), 64 * 1024));
         if (e != hipSuccess) {
@@ -830,7 +871,8 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
         (rc = upload(P.pack_src, &t->d_psrc)) != DF_OK || (rc = upload(t->tdst, &t->d_tdst)) != DF_OK ||
         (rc = upload(t->tsrc, &t->d_tsrc)) != DF_OK || (rc = upload(P.spack_dst, &t->d_sdst)) != DF_OK ||
         (rc = upload(P.spack_src, &t->d_ssrc)) != DF_OK || (rc = upload(P.wspack_dst, &t->d_wsdst)) != DF_OK ||
-        (rc = upload(P.wspack_src, &t->d_wssrc)) != DF_OK) {
+        (rc = upload(P.wspack_src, &t->d_wssrc)) != DF_OK || (rc = upload(t->lsblob, &t->d_lsblob)) != DF_OK ||
+        (rc = upload(t->lsdst, &t->d_lsdst)) != DF_OK || (rc = upload(t->lssrc, &t->d_lssrc)) != DF_OK) {
         std::string m = last_error();
         df_train_destroy(t);
         return set_err(rc, m);
