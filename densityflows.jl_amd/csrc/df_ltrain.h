@@ -33,6 +33,7 @@ constexpr int kLChunkBytes = 32 * 1024;  // weight chunk (LDS, double-buffered)
 #endif
 constexpr int kLTiles = DF_LTILES;       // 16-sample tiles per wave per round
 constexpr size_t kLdwLdsMax = 80 * 1024; // dW staging LDS (32 or 64 samples per step)
+constexpr size_t kLdwSplitLds = 2 * 3 * 256 * 80;  // SPLIT dW: both operands' planes, [p][row][32 samples + pad]
 constexpr int kLdwBM = 8;                // per-wave output blocks (16×16): up to 8 row tiles
 constexpr int kLdwBN = 4;                //   × 4 column tiles (128 accumulator registers)
 
@@ -88,6 +89,7 @@ struct LdwArgs {
     int64_t p_total;
     int w_off, b_off;       // trainables offsets (b_off -1: no bias)
     int64_t batch;
+    int split;              // 1: bf16x3 split products (ldw_split_body; mta = ntb = 16)
 };
 
 // One merged launch: up to three dW products (ldw) of net i and, optionally, the

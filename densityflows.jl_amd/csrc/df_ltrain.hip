@@ -611,10 +611,134 @@ __device__ __forceinline__ void ldw_body(const LdwArgs& a, float* lsm, int bid, 
     }
 }
 
+// dW = δ·inᵀ of a 256×256 Dense on bf16x3 split products (LdwArgs::split): each
+// staging step of 32 samples writes both operands to LDS as planes [p][row][sample]
+// (80-byte rows: the 16 rows × 4 lane groups of a ds_read_b128 hit 64 distinct banks),
+// split once per element; a wave's 8 × 4 blocks of 16×16 then take six bf16 MFMAs per
+// block and step (k = 32 samples).  A thread stages (row, 8 samples) items of both
+// operands (8 strided dword loads per item, lanes on consecutive rows: coalesced),
+// loaded one step ahead, and keeps the f32 sum of its δ items for db.
+__device__ __forceinline__ void ldw_split_body(const LdwArgs& a, uint8_t* lsm, int bid, int nblk) {
+    constexpr int RS = 80;                       // bytes per staged row (32 bf16 + pad)
+    constexpr int PB = 256 * RS;                 // bytes per plane
+    uint8_t* TA = lsm;                           // δ planes
+    uint8_t* TB = lsm + 3 * PB;                  // in planes
+    float* dbr = reinterpret_cast<float*>(lsm);  // db reduction (after the last step)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, j = lane & 15;
+    const int wi = wave % a.wm, wj = wave / a.wm;
+    const int m0 = wi * a.bm, n0 = wj * a.bn;
+    const int64_t per = (a.batch + nblk - 1) / nblk;
+    const int64_t s_begin = (int64_t)bid * per;
+    const int64_t s_end = (s_begin + per < a.batch) ? s_begin + per : a.batch;
+
+    f32x4 acc[kLdwBM][kLdwBN];
+#pragma unroll
+    for (int im = 0; im < kLdwBM; ++im)
+#pragma unroll
+        for (int in = 0; in < kLdwBN; ++in) acc[im][in] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // staging items: q = tid + k·512, k < 2 → operand A (1024 items: row q & 255, samples 8(q >> 8)..),
+    // k >= 2 → operand B; 4 items per thread, each 8 samples of one row
+    float pv[4][8];
+    float dbp[2] = {0.f, 0.f};
+    auto fetch = [&](int64_t s0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = (tid + (k & 1) * kBlockThreads);
+            const int row = q & 255, sg = q >> 8;
+            const float* src = (k < 2) ? a.da : a.xb;
+            const int ld = (k < 2) ? a.lda : a.ldb;
+            const int rmax = (k < 2) ? a.m_true : a.n_true;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int64_t smp = s0 + 8 * sg + e;
+                pv[k][e] = (smp < s_end && row < rmax) ? src[smp * ld + row] : 0.f;
+            }
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int q = (tid + (k & 1) * kBlockThreads);
+            const int row = q & 255, sg = q >> 8;
+            uni::bf16x8 x0, x1, x2;
+            uni::split8(pv[k], x0, x1, x2);
+            uint8_t* base = ((k < 2) ? TA : TB) + row * RS + 16 * sg;
+            *reinterpret_cast<uni::bf16x8*>(base) = x0;
+            *reinterpret_cast<uni::bf16x8*>(base + PB) = x1;
+            *reinterpret_cast<uni::bf16x8*>(base + 2 * PB) = x2;
+            if (k < 2) {  // db: this thread's 8 samples of row q & 255, in sample order
+                float sum = dbp[k];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sum = sum + pv[k][e];
+                dbp[k] = sum;
+            }
+        }
+    };
+
+    if (s_begin < s_end) fetch(s_begin);
+    for (int64_t s0 = s_begin; s0 < s_end; s0 += 32) {
+        __syncthreads();  // previous step consumed
+        stash();
+        __syncthreads();
+        if (s0 + 32 < s_end) fetch(s0 + 32);
+        // B planes of this wave's column blocks (rows 16(n0 + in) + j, samples 8g..8g+7)
+        uni::bf16x8 xb[kLdwBN][3];
+#pragma unroll
+        for (int in = 0; in < kLdwBN; ++in)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                xb[in][p] = *reinterpret_cast<const uni::bf16x8*>(TB + p * PB + (16 * (n0 + in) + j) * RS + 16 * g);
+#pragma unroll
+        for (int im = 0; im < kLdwBM; ++im) {
+            uni::bf16x8 wa[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                wa[p] = *reinterpret_cast<const uni::bf16x8*>(TA + p * PB + (16 * (m0 + im) + j) * RS + 16 * g);
+#pragma unroll
+            for (int in = 0; in < kLdwBN; ++in) {  // small terms first
+                f32x4 v = acc[im][in];
+                v = uni::mfma_bf(wa[2], xb[in][0], v);
+                v = uni::mfma_bf(wa[1], xb[in][1], v);
+                v = uni::mfma_bf(wa[0], xb[in][2], v);
+                v = uni::mfma_bf(wa[1], xb[in][0], v);
+                v = uni::mfma_bf(wa[0], xb[in][1], v);
+                acc[im][in] = uni::mfma_bf(wa[0], xb[in][0], v);
+            }
+        }
+    }
+
+    float* dst = a.partial + (int64_t)bid * a.p_total;
+#pragma unroll
+    for (int im = 0; im < kLdwBM; ++im) {
+        const int ma = m0 + im;
+#pragma unroll
+        for (int in = 0; in < kLdwBN; ++in) {
+            const int nbk = n0 + in;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * ma + 4 * g + r, col = 16 * nbk + j;
+                if (row < a.m_true && col < a.n_true) dst[a.w_off + row + (int64_t)a.m_true * col] = acc[im][in][r];
+            }
+        }
+    }
+    // db[row] = Σ over the workgroup's samples: the four sample groups of a row in order
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) dbr[tid + k * kBlockThreads] = dbp[k];
+    __syncthreads();
+    if (a.b_off >= 0 && tid < a.m_true) {
+        const float v = ((dbr[tid] + dbr[tid + 256]) + dbr[tid + 512]) + dbr[tid + 768];
+        dst[a.b_off + tid] = v;
+    }
+}
+
 template <int S, int BMX, int BNX>
 __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lsm[];
-    ldw_body<S, BMX, BNX>(a, lsm, blockIdx.x, gridDim.x);
+    if (a.split) ldw_split_body(a, reinterpret_cast<uint8_t*>(lsm), blockIdx.x, gridDim.x);
+    else ldw_body<S, BMX, BNX>(a, lsm, blockIdx.x, gridDim.x);
 }
 
 // One merged launch of the sweep: the dW products of net i (each workgroup's
@@ -634,7 +758,9 @@ __global__ void __launch_bounds__(kBlockThreads, 1) sweep_kernel(SweepJob j) {
         }
     }
     for (int k = 0; k < j.nw; ++k) {
-        if (j.ws[k] == 64)
+        if (j.w[k].split)
+            ldw_split_body(j.w[k], smem, blockIdx.x, gridDim.x);
+        else if (j.ws[k] == 64)
             ldw_body<64, 2, 2>(j.w[k], reinterpret_cast<float*>(smem), blockIdx.x, gridDim.x);
         else
             ldw_body<32, kLdwBM, kLdwBN>(j.w[k], reinterpret_cast<float*>(smem), blockIdx.x, gridDim.x);
@@ -768,7 +894,7 @@ static size_t ldw_stage_bytes(int S, int mta, int ntb) { return (size_t)S * (16 
 static int ldw_samples(const LdwArgs& a) {
     return (a.bm <= 2 && a.bn <= 2 && ldw_stage_bytes(64, a.mta, a.ntb) <= kLdwLdsMax) ? 64 : 32;
 }
-size_t ldw_lds_bytes() { return kLdwLdsMax; }
+size_t ldw_lds_bytes() { return kLdwSplitLds > kLdwLdsMax ? kLdwSplitLds : kLdwLdsMax; }
 
 bool ldw_shape(int mta, int ntb, int* wm, int* bm, int* bn) {
     int best = 1 << 30;
@@ -814,7 +940,8 @@ hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st) {
     const int S = ldw_samples(a);
     void* fn = S == 64 ? reinterpret_cast<void*>(&ldw_kernel<64, 2, 2>)
                        : reinterpret_cast<void*>(&ldw_kernel<32, kLdwBM, kLdwBN>);
-    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, ldw_stage_bytes(S, a.mta, a.ntb), st);
+    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args,
+                           a.split ? kLdwSplitLds : ldw_stage_bytes(S, a.mta, a.ntb), st);
 }
 
 }  // namespace df

@@ -605,6 +605,8 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             w.b_off = D.b_off;
             w.batch = batch;
             if (!ldw_shape(w.mta, w.ntb, &w.wm, &w.bm, &w.bn)) return set_err(DF_ERR_UNSUPPORTED, "dW tiling");
+            // hidden-256 × hidden-256 dW on bf16x3 split products (ldw_split_body)
+            w.split = (lsplit && w.mta == 16 && w.ntb == 16 && w.bm == kLdwBM && w.bn == kLdwBN) ? 1 : 0;
             out.push_back(w);
         }
         return DF_OK;
