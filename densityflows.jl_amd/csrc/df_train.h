@@ -50,6 +50,15 @@ struct GNet {
     int64_t t_src;           // byte offset of the transposed region in the training blob
     int32_t p_begin, p_count;          // the net's contiguous slice of the trainables
     int32_t w_off[3], b_off[3];        // first Dense, hidden Dense, output Dense (b_off -1: no bias)
+    // SPLIT (chain plan.split, hidden 32/64, relu): the recompute runs on the net's
+    // region of the chain's SPLIT blob (bitwise the inverse pass), W1ᵀδ and dW1 on
+    // bf16x3 products; W1ᵀ planes [c][m][p][lane][8] in the trainer's split blob
+    int32_t split;
+    UNet su;                 // SPLIT forward region offsets (rebased to the net's LDS copy)
+    int32_t sfwd_bytes;
+    int64_t sfwd_src;        // byte offset of the net's region in the chain's SPLIT blob
+    int32_t st_bytes;
+    int64_t st_src;          // byte offset of its W1ᵀ planes in the trainer's split blob
 };
 
 enum : int { TR_PHASE_S = 0, TR_PHASE_T = 1 };
@@ -67,6 +76,8 @@ struct TrainArgs {
     float* partial;          // [workgroup][p_total] gradient partials
     const uint8_t* blob;     // chain weight blob (forward fragments)
     const uint8_t* tblob;    // transposed fragments
+    const uint8_t* sblob;    // SPLIT: the chain's SPLIT blob (forward region of the net)
+    const uint8_t* tsblob;   // SPLIT: the trainer's W1ᵀ planes
     int64_t batch;
     int64_t p_total;
     int d, n, n_af, kind, phase;
@@ -78,7 +89,7 @@ size_t train_net_lds(int ht, const GNet& g);
 hipError_t set_train_lds_limit(size_t lds);
 hipError_t launch_train_net(int ht, int nh, int am, const TrainArgs& a, unsigned grid, size_t lds,
                             hipStream_t st);
-hipError_t train_net_occupancy(int ht, int nh, int am, size_t lds, int* blocks);
+hipError_t train_net_occupancy(int ht, int nh, int am, size_t lds, int* blocks, bool split = false);
 
 hipError_t launch_scale(float* dst, const float* src, float s, int64_t count, hipStream_t st);
 hipError_t launch_norm_adjoint(float* zbar, const float* xmin, const float* xmax, float alpha, float beta, int d,

@@ -8,7 +8,13 @@ namespace df {
 
 namespace {
 
-void* train_ptr(int ht, int nh, int am) {
+void* train_ptr(int ht, int nh, int am, bool split = false) {
+    if (split) {
+        if (nh != 1 || am != trn::AM_RELU) return nullptr;
+        if (ht == 2) return train_kernel_ptr<2, 1, trn::AM_RELU, true>();
+        if (ht == 4) return train_kernel_ptr<4, 1, trn::AM_RELU, true>();
+        return nullptr;
+    }
 #define DF_T(H)                                                                                           \
     (nh ? (am == trn::AM_RELU ? train_kernel_ptr<H, 1, trn::AM_RELU>()                                   \
                               : (am == trn::AM_PRE ? train_kernel_ptr<H, 1, trn::AM_PRE>()                \
@@ -120,6 +126,7 @@ unsigned blocks_for(int64_t count, int threads) { return (unsigned)((count + thr
 size_t train_net_lds(int ht, const GNet& g) {
     const size_t tarea = (size_t)kWavesPerBlock * 2 * 16 * ht * kTS * 4;
     const size_t red = (size_t)g.p_count * 4;
+    if (g.split) return (size_t)g.sfwd_bytes + ht * 1024 + g.st_bytes + (tarea > red ? tarea : red);
     return (size_t)g.fwd_bytes + g.t_bytes + (tarea > red ? tarea : red);
 }
 
@@ -131,19 +138,24 @@ hipError_t set_train_lds_limit(size_t lds) {
                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 if (e != hipSuccess) return e;
             }
+    for (int ht : {2, 4}) {
+        hipError_t e = hipFuncSetAttribute(train_ptr(ht, 1, trn::AM_RELU, true),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
     return hipSuccess;
 }
 
 hipError_t launch_train_net(int ht, int nh, int am, const TrainArgs& a, unsigned grid, size_t lds,
                             hipStream_t st) {
-    void* k = train_ptr(ht, nh, am);
+    void* k = train_ptr(ht, nh, am, a.net.split != 0);
     if (!k) return hipErrorInvalidValue;
     void* args[] = {const_cast<TrainArgs*>(&a)};
     return hipLaunchKernel(k, dim3(grid), dim3(kBlockThreads), args, lds, st);
 }
 
-hipError_t train_net_occupancy(int ht, int nh, int am, size_t lds, int* blocks) {
-    void* k = train_ptr(ht, nh, am);
+hipError_t train_net_occupancy(int ht, int nh, int am, size_t lds, int* blocks, bool split) {
+    void* k = train_ptr(ht, nh, am, split);
     if (!k) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k, kBlockThreads, lds);
 }

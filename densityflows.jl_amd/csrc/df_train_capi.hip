@@ -116,6 +116,11 @@ struct df_train {
     std::vector<LNet> lnets;
     std::vector<uint8_t> lblob;      // fragments (W and Wᵀ) then padded biases
     std::vector<int32_t> ldst, lsrc; // repack map (float index ← trainables index)
+    std::vector<uint8_t> tsblob;     // SPLIT W1ᵀ planes of the fused path (GNet::st_src)
+    std::vector<int32_t> tsdst, tssrc; // repack map (byte offset ← trainables index·4 + plane)
+    void* d_tsblob = nullptr;
+    void* d_tsdst = nullptr;
+    void* d_tssrc = nullptr;
     std::vector<uint8_t> lsblob;     // SPLIT planes of the layer-wise Wᵀ operands (LOp::sfrag)
     std::vector<int32_t> lsdst, lssrc; // repack map (byte offset ← trainables index·4 + plane)
     void* d_lsblob = nullptr;
@@ -167,7 +172,8 @@ void free_all(df_train* t) {
                     t->d_psrc,   t->d_tdst, t->d_tsrc, t->d_snap, t->d_zbar,    t->d_ebuf,  t->d_lpsum,
                     t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_lyp[0], t->d_lyp[1], t->d_lbp[0], t->d_lbp[1], t->d_lx, t->d_hsave,
                     t->d_wdst,   t->d_wsrc, t->d_wbdst, t->d_wbsrc, t->d_sdst, t->d_ssrc,
-                    t->d_wsdst, t->d_wssrc, t->d_lsblob, t->d_lsdst, t->d_lssrc};
+                    t->d_wsdst, t->d_wssrc, t->d_lsblob, t->d_lsdst, t->d_lssrc,
+                    t->d_tsblob, t->d_tsdst, t->d_tssrc};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (float* p : t->d_lh)
@@ -377,6 +383,41 @@ int build_nets(df_train* t) {
             }
             g.p_count = end - g.p_begin;
             pack_transposed(t, P, g, D0, D1, ht);
+            // SPLIT: the net's region of the chain's SPLIT blob and its W1ᵀ planes
+            const char* ex = std::getenv("DF_F32_EXACT");
+            if (P.split && D1 && t->amode == trn::AM_RELU && (ht == 2 || ht == 4) && !(ex && ex[0] == '1')) {
+                const ULayer& SU = P.sulayers[li];
+                const UNet& s0 = (phase == TR_PHASE_S) ? SU.s : SU.t;
+                const int slo = s0.off_w0;
+                const int shi = s0.off_out + round16((s0.n_out * 16 * ht + 4) * 4);
+                g.split = 1;
+                g.su = s0;
+                g.su.off_w0 -= slo;
+                g.su.off_h -= slo;
+                g.su.off_out -= slo;
+                g.sfwd_src = P.sstages[s0.stage].src_off + slo;
+                g.sfwd_bytes = round16(shi - slo);
+                g.st_src = (int64_t)t->tsblob.size();
+                g.st_bytes = (ht / 2) * ht * 3072;
+                t->tsblob.resize(t->tsblob.size() + g.st_bytes, 0);
+                const int h = g.h_true;
+                for (int c = 0; c < ht / 2; ++c)
+                    for (int m = 0; m < ht; ++m)
+                        for (int p = 0; p < 3; ++p)
+                            for (int lane = 0; lane < 64; ++lane)
+                                for (int e = 0; e < 8; ++e) {
+                                    const int i = 16 * m + (lane & 15), gg = lane >> 4;
+                                    const int k = 32 * c + 16 * (e >> 2) + 4 * gg + (e & 3);
+                                    if (i >= h || k >= h) continue;
+                                    const int64_t src = D1->w_off + k + (int64_t)h * i;  // W1ᵀ[i, k] = W1[k, i]
+                                    const int64_t at =
+                                        g.st_src + ((((int64_t)c * ht + m) * 3 + p) * 64 + lane) * 16 + 2 * e;
+                                    const uint16_t hv = bf16_split_plane(P.trainables[src], p);
+                                    std::memcpy(&t->tsblob[at], &hv, 2);
+                                    t->tsdst.push_back((int32_t)at);
+                                    t->tssrc.push_back((int32_t)(src * 4 + p));
+                                }
+            }
             t->nets.push_back(g);
             t->net_nh.push_back(u0.nh);
             t->ops.push_back({li, (int)t->nets.size() - 1, phase});
@@ -482,6 +523,9 @@ int repack(df_train* t, hipStream_t st) {
     if (e == hipSuccess && !t->ldst.empty())
         e = launch_repack(static_cast<float*>(t->d_lblob), static_cast<const int32_t*>(t->d_ldst),
                           static_cast<const int32_t*>(t->d_lsrc), (int64_t)t->ldst.size(), t->d_params, st);
+    if (e == hipSuccess && !t->tsdst.empty())
+        e = launch_repack_split(static_cast<uint8_t*>(t->d_tsblob), static_cast<const int32_t*>(t->d_tsdst),
+                                static_cast<const int32_t*>(t->d_tssrc), (int64_t)t->tsdst.size(), t->d_params, st);
     if (e == hipSuccess && !t->lsdst.empty())
         e = launch_repack_split(static_cast<uint8_t*>(t->d_lsblob), static_cast<const int32_t*>(t->d_lsdst),
                                 static_cast<const int32_t*>(t->d_lssrc), (int64_t)t->lsdst.size(), t->d_params, st);
@@ -805,6 +849,9 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
         t->tblob.clear();
         t->tdst.clear();
         t->tsrc.clear();
+        t->tsblob.clear();
+        t->tsdst.clear();
+        t->tssrc.clear();
         t->layerwise = true;
         rc = build_lnets(t);
     }
@@ -832,7 +879,8 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
     int occ = 1;
     for (size_t i = 0; i < t->nets.size(); ++i) {
         int b = 1;
-        if (train_net_occupancy(P.ht, t->net_nh[i], t->amode, t->lds_max, &b) == hipSuccess && b >= 1)
+        if (train_net_occupancy(P.ht, t->net_nh[i], t->amode, t->lds_max, &b, t->nets[i].split != 0) == hipSuccess &&
+            b >= 1)
             occ = (i == 0) ? b : std::min(occ, b);
     }
     t->grid = std::max(1, c->n_cu * occ);
@@ -874,7 +922,9 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
         (rc = upload(t->tsrc, &t->d_tsrc)) != DF_OK || (rc = upload(P.spack_dst, &t->d_sdst)) != DF_OK ||
         (rc = upload(P.spack_src, &t->d_ssrc)) != DF_OK || (rc = upload(P.wspack_dst, &t->d_wsdst)) != DF_OK ||
         (rc = upload(P.wspack_src, &t->d_wssrc)) != DF_OK || (rc = upload(t->lsblob, &t->d_lsblob)) != DF_OK ||
-        (rc = upload(t->lsdst, &t->d_lsdst)) != DF_OK || (rc = upload(t->lssrc, &t->d_lssrc)) != DF_OK) {
+        (rc = upload(t->lsdst, &t->d_lsdst)) != DF_OK || (rc = upload(t->lssrc, &t->d_lssrc)) != DF_OK ||
+        (rc = upload(t->tsblob, &t->d_tsblob)) != DF_OK || (rc = upload(t->tsdst, &t->d_tsdst)) != DF_OK ||
+        (rc = upload(t->tssrc, &t->d_tssrc)) != DF_OK) {
         std::string m = last_error();
         df_train_destroy(t);
         return set_err(rc, m);
@@ -966,6 +1016,8 @@ int df_train_gradient(df_train* t, const float* x, const float* theta_raw, int64
         a.partial = t->d_partial;
         a.blob = static_cast<const uint8_t*>(c->d_blob);
         a.tblob = static_cast<const uint8_t*>(t->d_tblob);
+        a.sblob = static_cast<const uint8_t*>(c->d_sblob);
+        a.tsblob = static_cast<const uint8_t*>(t->d_tsblob);
         a.batch = batch;
         a.p_total = t->P;
         a.d = P.d;

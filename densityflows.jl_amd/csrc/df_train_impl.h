@@ -104,17 +104,40 @@ __device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)
 
 }  // namespace trn
 
-template <int HT, int NH, int AM>
+// bf16x4 halves of the SPLIT dW1 operands (4 samples of one row, one plane)
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split4(f32x4 v, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const __bf16 h = (__bf16)v[e];
+        const float r = v[e] - (float)h;
+        const __bf16 m = (__bf16)r;
+        p0[e] = h;
+        p1[e] = m;
+        p2[e] = (__bf16)(r - (float)m);
+    }
+}
+
+__device__ __forceinline__ uni::bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int HT, int NH, int AM, bool SPLIT = false>
 __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a) {
     using namespace trn;
     constexpr bool RELU = (AM == AM_RELU);
     constexpr bool PRE = (AM == AM_PRE);
+    static_assert(!SPLIT || (RELU && NH == 1 && HT >= 2), "SPLIT: relu nets with one hidden Dense, hidden 32/64");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const GNet& G = a.net;
-    const UNet& N = G.u;
+    const UNet& N = SPLIT ? G.su : G.u;
+    const int fwd_bytes = SPLIT ? G.sfwd_bytes : G.fwd_bytes;
+    const int t_bytes = SPLIT ? HT * 1024 : G.t_bytes;  // SPLIT: W0ᵀ only (W1ᵀ as planes)
     uint8_t* fw = smem;
-    uint8_t* tw = smem + G.fwd_bytes;
-    float* tarea = reinterpret_cast<float*>(smem + G.fwd_bytes + G.t_bytes);
+    uint8_t* tw = smem + fwd_bytes;
+    uint8_t* stw = tw + t_bytes;
+    float* tarea = reinterpret_cast<float*>(stw + (SPLIT ? G.st_bytes : 0));
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, j = lane & 15;
@@ -127,10 +150,14 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
     const bool rnvp = (a.kind == DF_LAYER_RNVP);
 
     {  // the net's forward and transposed fragments → LDS
-        const f32x4* src = reinterpret_cast<const f32x4*>(a.blob + G.fwd_src);
-        for (int i = tid; i < G.fwd_bytes / 16; i += kBlockThreads) reinterpret_cast<f32x4*>(fw)[i] = src[i];
+        const f32x4* src = reinterpret_cast<const f32x4*>(SPLIT ? a.sblob + G.sfwd_src : a.blob + G.fwd_src);
+        for (int i = tid; i < fwd_bytes / 16; i += kBlockThreads) reinterpret_cast<f32x4*>(fw)[i] = src[i];
         const f32x4* srt = reinterpret_cast<const f32x4*>(a.tblob + G.t_src);
-        for (int i = tid; i < G.t_bytes / 16; i += kBlockThreads) reinterpret_cast<f32x4*>(tw)[i] = srt[i];
+        for (int i = tid; i < t_bytes / 16; i += kBlockThreads) reinterpret_cast<f32x4*>(tw)[i] = srt[i];
+        if constexpr (SPLIT) {
+            const f32x4* sst = reinterpret_cast<const f32x4*>(a.tsblob + G.st_src);
+            for (int i = tid; i < G.st_bytes / 16; i += kBlockThreads) reinterpret_cast<f32x4*>(stw)[i] = sst[i];
+        }
     }
     // zero rows of the δ_out transpose that no lane writes (rows >= 4)
     for (int i = lane; i < TROWS * kTS; i += 64) TA[i] = 0.f;
@@ -244,15 +271,24 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
         f32x4 A0[1][HT], A1[1][HT];
         constexpr int NP = PRE ? HT : 1;
         f32x4 D0[NP], D1[NP];  // AM_PRE: σ'(pre) of the first / hidden Dense
-        uni::dense_first<HT, 1>(fw, N, xin, A0);
-        if constexpr (PRE) {
+        if constexpr (SPLIT) {  // the inverse pass's SPLIT kernel functions: bitwise its s and t
+            uni::dense_first_split<HT, 1>(fw, N, xin, A0);
+            uni::bias_act<HT, 1, true>(fw, DF_ACT_RELU, A0, false);
+        } else {
+            uni::dense_first<HT, 1>(fw, N, xin, A0);
+        }
+        if constexpr (SPLIT) {
+        } else if constexpr (PRE) {
             uni::bias_act<HT, 1, false>(fw + N.off_b0, DF_ACT_IDENTITY, A0, !N.fold0);
             act_keep_grad<HT>(N.act0, A0[0], D0);
         } else {
             uni::bias_act<HT, 1, RELU>(fw + N.off_b0, N.act0, A0, !N.fold0);
         }
         load_pull(s, valid, zbp, aux);
-        if constexpr (NH == 1) {
+        if constexpr (SPLIT) {
+            uni::dense_hidden_split<HT, 1, true, true>(fw + N.off_h, A0, A1);
+            uni::bias_act<HT, 1, true>(fw, DF_ACT_RELU, A1, false);
+        } else if constexpr (NH == 1) {
             uni::dense_hidden<HT, 1>(fw + N.off_h, A0, A1);
             if constexpr (PRE) {
                 uni::bias_act<HT, 1, false>(fw + N.off_h + HT * HT * 1024, DF_ACT_IDENTITY, A1);
@@ -358,14 +394,36 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
                 fb[m] = lds4f(TB + (16 * m + j) * kTS + 4 * g);
                 gbh[m] += hsum4(fa[m]);
             }
+            if constexpr (SPLIT) {
+                // k-slot (g, e) of MFMA u: sample 4g + (e & 3), product 2u + (e >> 2) of
+                // (w0x0, w0x1 | w1x0, w0x2 | w1x1, w2x0), δ rows as A, A0 rows as B
+                bf16x4 pb[HT][3];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+                for (int m = 0; m < HT; ++m) split4(fb[m], pb[m][0], pb[m][1], pb[m][2]);
 #pragma unroll
-                for (int ma = 0; ma < HT; ++ma)
+                for (int ma = 0; ma < HT; ++ma) {
+                    bf16x4 pa[3];
+                    split4(fa[ma], pa[0], pa[1], pa[2]);
+                    const uni::bf16x8 a0 = cat8(pa[1], pa[2]), a1 = cat8(pa[1], pa[0]), a2 = cat8(pa[0], pa[0]);
 #pragma unroll
-                    for (int mb = 0; mb < HT; ++mb) gWh[ma][mb] = mfma4(fa[ma][q], fb[mb][q], gWh[ma][mb]);
+                    for (int mb = 0; mb < HT; ++mb) {  // small terms first
+                        f32x4 v = gWh[ma][mb];
+                        v = uni::mfma_bf(a0, cat8(pb[mb][1], pb[mb][0]), v);
+                        v = uni::mfma_bf(a1, cat8(pb[mb][0], pb[mb][2]), v);
+                        gWh[ma][mb] = uni::mfma_bf(a2, cat8(pb[mb][0], pb[mb][1]), v);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int ma = 0; ma < HT; ++ma)
+#pragma unroll
+                        for (int mb = 0; mb < HT; ++mb) gWh[ma][mb] = mfma4(fa[ma][q], fb[mb][q], gWh[ma][mb]);
+            }
             load_zx(s, valid, zxp);
-            uni::dense_hidden<HT, 1>(tw + G.off_ht, hb, d0);
+            if constexpr (SPLIT) uni::dense_hidden_split<HT, 1, false, true>(stw, hb, d0);
+            else uni::dense_hidden<HT, 1>(tw + G.off_ht, hb, d0);
             if constexpr (PRE) {
 #pragma unroll
                 for (int m = 0; m < HT; ++m) d0[0][m] = d0[0][m] * D0[m];
@@ -468,9 +526,9 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
     for (int i = tid; i < G.p_count; i += kBlockThreads) dst[i] = R[i];
 }
 
-template <int HT, int NH, int AM>
+template <int HT, int NH, int AM, bool SPLIT = false>
 void* train_kernel_ptr() {
-    return reinterpret_cast<void*>(&train_net_kernel<HT, NH, AM>);
+    return reinterpret_cast<void*>(&train_net_kernel<HT, NH, AM, SPLIT>);
 }
 
 }  // namespace df

@@ -425,7 +425,8 @@ __device__ __forceinline__ void dense_first_split(const uint8_t* buf, const UNet
 // (g, j): rows 32c + 16(e>>2) + 4g + (e&3) of sample j), split on the fly.
 // The accumulators start from the bias (b + W·x: the sum's rounding order differs
 // from Flux's W*x .+ b by one f32 rounding, like any other summation order).
-template <int HT, int TT>
+// BIAS false (the training kernel's W1ᵀδ): the chains start from zero.
+template <int HT, int TT, bool BIAS = true, bool FENCE = false>
 __device__ __forceinline__ void dense_hidden_split(const uint8_t* wb, const f32x4 (&in)[TT][HT],
                                                    f32x4 (&out)[TT][HT]) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
@@ -433,7 +434,7 @@ __device__ __forceinline__ void dense_hidden_split(const uint8_t* wb, const f32x
     wb += lane * 16;
 #pragma unroll
     for (int m = 0; m < HT; ++m) {
-        const f32x4 b = lds4(bb + ((16 * m + 4 * g) << 2));
+        const f32x4 b = BIAS ? lds4(bb + ((16 * m + 4 * g) << 2)) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < TT; ++t) out[t][m] = b;
     }
@@ -462,6 +463,7 @@ __device__ __forceinline__ void dense_hidden_split(const uint8_t* wb, const f32x
                 a = mfma_bf(w0, x[t][1], a);
                 out[t][m] = mfma_bf(w0, x[t][0], a);
             }
+            if (FENCE) asm volatile("" ::: "memory");  // fragment reads not hoisted past this m-tile
         }
     }
 }
