@@ -54,6 +54,70 @@ def test_plan_config2_and_config1():
     assert info.n_params == 2322 and info.flops_per_sample == 4224.0 and info.n_stages == 1
 
 
+@pytest.mark.parametrize("exact", ["0", "1"])
+def test_plan_kernel_choice_split(monkeypatch, exact):
+    """Config 2 plans the FAST SPLIT kernel (id 4), config 4 the wide SPLIT kernel
+    (id 6), config 1 (hidden 16) the exact FAST kernel (id 3); DF_F32_EXACT=1 plans
+    the exact-f32 kernels.  split_flops_per_sample is the FLOP the SPLIT kernels run
+    as bf16x3 products: first + hidden Dense of every net at config 2, all three
+    Denses at config 4."""
+    monkeypatch.setenv("DF_F32_EXACT", exact)
+    rng = np.random.default_rng(0)
+    ch2 = dfa.FlowChain.repeat(dfa.CouplingBlock, 4, 5, hidden_dim_s=64, hidden_dim_t=64, rng=rng)
+    i2 = hip.validate(ch2.layers)
+    ch4 = dfa.FlowChain.repeat(dfa.CouplingBlock, 8, 32, n=8, hidden_dim_s=256, hidden_dim_t=256, rng=rng)
+    i4 = hip.validate(ch4.layers)
+    ch1 = dfa.FlowChain.repeat(dfa.CouplingBlock, 2, 5, hidden_dim_s=16, hidden_dim_t=16, rng=rng)
+    i1 = hip.validate(ch1.layers)
+    if exact == "1":
+        assert (i2.kernel, i4.kernel, i1.kernel) == (3, 5, 3)
+        assert i2.split_flops_per_sample == i4.split_flops_per_sample == 0.0
+    else:
+        assert (i2.kernel, i4.kernel, i1.kernel) == (4, 6, 3)
+        # per net 2·(in·64 + 64·64), in = 2 or 3 (the 64·out output GEMV stays f32)
+        want2 = sum(2.0 * (inn * 64 + 64 * 64) for inn in (2, 3) * 4 for _net in (0, 1))
+        assert i2.split_flops_per_sample == want2
+        assert i4.split_flops_per_sample == i4.flops_per_sample
+
+
+def _bf16_rne(v):
+    """f32 → bf16 bits by round-to-nearest-even (df_plan.h bf16_rne_bits), as f32."""
+    u = np.asarray(v, np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32)
+
+
+def test_bf16x3_split_is_exact_and_six_products_are_f32_accurate():
+    """The SPLIT arithmetic, restated in numpy: three RNE bf16 planes
+    sum exactly to the f32 value, and the six kept products w0x0 + w0x1 + w1x0 +
+    w0x2 + w1x1 + w2x0 (each exact in f32) differ from w·x by less than 2^-24·|w·x|."""
+    rng = np.random.default_rng(5)
+    w = (rng.standard_normal(200000) * np.exp(rng.uniform(-20, 20, 200000))).astype(np.float32)
+    x = (rng.standard_normal(200000) * np.exp(rng.uniform(-20, 20, 200000))).astype(np.float32)
+
+    def planes(a):
+        p0 = _bf16_rne(a)
+        r = (a - p0).astype(np.float32)
+        p1 = _bf16_rne(r)
+        p2 = _bf16_rne((r - p1).astype(np.float32))
+        return p0, p1, p2
+
+    w0, w1, w2 = planes(w)
+    x0, x1, x2 = planes(x)
+    for a, (a0, a1, a2) in ((w, (w0, w1, w2)), (x, (x0, x1, x2))):
+        np.testing.assert_array_equal(a0.astype(np.float64) + a1 + a2, a.astype(np.float64))
+    d = np.float64
+    six = (w0.astype(d) * x0 + w0.astype(d) * x1 + w1.astype(d) * x0 + w0.astype(d) * x2
+           + w1.astype(d) * x1 + w2.astype(d) * x0)
+    exact = w.astype(d) * x.astype(d)
+    rel = np.abs(six - exact) / np.abs(exact)
+    assert rel.max() < 2.0 ** -24, rel.max()
+    # every bf16 product is exact in f32 (8 + 8 significand bits)
+    for a, b in ((w0, x0), (w0, x1), (w2, x0)):
+        p = a.astype(d) * b.astype(d)
+        np.testing.assert_array_equal(p.astype(np.float32).astype(d), p)
+
+
 def test_plan_config4():
     rng = np.random.default_rng(0)
     ch4 = dfa.FlowChain.repeat(dfa.CouplingBlock, 8, 32, n=8, hidden_dim_s=256, hidden_dim_t=256, rng=rng)
