@@ -61,8 +61,28 @@ struct WStager {
     int idx;
     int cur;
     int bytes;  // ring slot size: kWideStageBytes, or kWideSplitStageBytes (SPLIT)
+    // staggered DMA (SPLIT): this wave's pieces of the next stage, issued one per
+    // m-tile by split_chunk instead of all at the stage switch
+    const uint8_t* blob;
+    int psrc;   // byte offset of the pending stage in the blob
+    int pdst;   // its ring slot's byte offset from base
+    int pnext, pend;
     __device__ __forceinline__ uint8_t* buf() const { return slot(idx); }
     __device__ __forceinline__ uint8_t* slot(int i) const { return base + (i % kWideBufs) * bytes; }
+    template <int NW>
+    __device__ __forceinline__ void issue_one() {
+        if (pnext < pend) {
+            const int lane = threadIdx.x & 63;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(blob + psrc + (pnext << 10) + lane * 16),
+                                             (__attribute__((address_space(3))) void*)(base + pdst + (pnext << 10)), 16,
+                                             0, 0);
+            pnext += NW;
+        }
+    }
+    template <int NW>
+    __device__ __forceinline__ void issue_all() {
+        while (pnext < pend) issue_one<NW>();
+    }
 };
 
 // DMA instructions wave w issues for a stage of `bytes` (1 KiB per instruction,
@@ -104,9 +124,10 @@ __device__ __forceinline__ void dma(const ChainArgs& a, int s, uint8_t* dst) {
 // Vector-memory loads return in order, so waiting until at most the newer
 // in-flight stages' DMA instructions of this wave are outstanding means this
 // wave's part of stage s has landed; the barrier then covers every wave's part.
-template <int NW = kWideWaves>
+template <int NW = kWideWaves, bool STAGGER = false>
 __device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
     if (s == sg.cur) return;
+    if (STAGGER) sg.issue_all<NW>();  // pieces of stage s not issued yet
     const int nidx = sg.idx + 1;
     if (kWideBufs > 2) {
         const int wave = threadIdx.x >> 6;
@@ -134,7 +155,17 @@ __device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
         sg.n = 0;
         return;
     }
-    if (nidx + kWideBufs - 1 < sg.n) dma<NW>(a, cref(sg.sched + nidx + kWideBufs - 1), sg.slot(nidx + kWideBufs - 1));
+    if (nidx + kWideBufs - 1 < sg.n) {
+        if (STAGGER) {
+            const DevStage& st = cref(a.stages + cref(sg.sched + nidx + kWideBufs - 1));
+            sg.psrc = (int)st.src_off;
+            sg.pdst = (int)(sg.slot(nidx + kWideBufs - 1) - sg.base);
+            sg.pnext = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            sg.pend = st.bytes >> 10;
+        } else {
+            dma<NW>(a, cref(sg.sched + nidx + kWideBufs - 1), sg.slot(nidx + kWideBufs - 1));
+        }
+    }
 }
 
 // h = σ.(acc .+ b)  (b: 256 floats in global memory, L2-resident)
@@ -305,6 +336,9 @@ using uni::split8;
 #endif
 constexpr int kSplitWaves = DF_WSPLIT_WAVES;         // 4: one wave per SIMD, 2 tiles; 8: two, 1 tile
 constexpr int kSplitT = 8 / DF_WSPLIT_WAVES;        // 128 samples per workgroup either way
+#ifndef DF_WIDE_STAGGER
+#define DF_WIDE_STAGGER 1
+#endif
 
 // acc += W·x over one 32-input chunk for m-tiles [0, MT): planes [m][p][lane][8] at
 // buf (lane offset applied), activation planes x[t][p]; the next m-tile's planes
@@ -320,7 +354,7 @@ constexpr int kSplitT = 8 / DF_WSPLIT_WAVES;        // 128 samples per workgroup
 //   !HILO (the one- or two-chunk first Dense): all six products onto hi.
 template <int TT, int MT, bool HILO, int MA>
 __device__ __forceinline__ void split_chunk(const uint8_t* buf, const bf16x8 (&x)[TT][3], f32x4 (&hi)[TT][MA],
-                                            f32x4 (&lo)[TT][MA]) {
+                                            f32x4 (&lo)[TT][MA], WStager& sg) {
     bf16x8 w[2][3];
 #pragma unroll
     for (int p = 0; p < 3; ++p) w[0][p] = *reinterpret_cast<const bf16x8*>(buf + p * 1024);
@@ -346,6 +380,7 @@ __device__ __forceinline__ void split_chunk(const uint8_t* buf, const bf16x8 (&x
                 hi[t][m] = mfma_bf(w[cb][0], x[t][0], v);
             }
         }
+        if (DF_WIDE_STAGGER) sg.issue_one<kSplitWaves>();  // one DMA piece of the next stage per m-tile
         asm volatile("" ::: "memory");  // fragment reads stay one m-tile ahead (no hoisting)
     }
 }
@@ -384,7 +419,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         if (c < N.nst0) {
-            ensure<kSplitWaves>(N.stage0 + c, sg, a);
+            ensure<kSplitWaves, DF_WIDE_STAGGER != 0>(N.stage0 + c, sg, a);
             bf16x8 x[TT][3];
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
@@ -393,7 +428,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
                 for (int e = 0; e < 8; ++e) v[e] = state[ro[t] + sfeat[32 * c + 8 * g + e]];
                 split8(v, x[t][0], x[t][1], x[t][2]);
             }
-            split_chunk<TT, 16, false>(sg.buf() + lane * 16, x, acc, acc);
+            split_chunk<TT, 16, false>(sg.buf() + lane * 16, x, acc, acc, sg);
         }
     }
 #pragma unroll
@@ -415,7 +450,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
     }
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        ensure<kSplitWaves>(N.stage0 + N.nst0 + c, sg, a);
+        ensure<kSplitWaves, DF_WIDE_STAGGER != 0>(N.stage0 + N.nst0 + c, sg, a);
         if (hs && c == 0) {  // training: keep H0 (as in eval_net)
 #pragma unroll
             for (int t = 0; t < TT; ++t)
@@ -426,7 +461,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
         }
         bf16x8 x[TT][3];
         split_tiles<TT>(h, c, x);
-        split_chunk<TT, 16, true>(sg.buf() + lane * 16, x, acc, lo);
+        split_chunk<TT, 16, true>(sg.buf() + lane * 16, x, acc, lo, sg);
     }
 #pragma unroll
     for (int t = 0; t < TT; ++t)
@@ -438,7 +473,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
         }
 
     // ---- output Dense (<= 32 outputs) ----
-    ensure<kSplitWaves>(N.stage0 + N.nst0 + 8, sg, a);
+    ensure<kSplitWaves, DF_WIDE_STAGGER != 0>(N.stage0 + N.nst0 + 8, sg, a);
     if (hs) {  // training: keep H1
         float* hs1 = hs + a.batch * a.hsave_w;
 #pragma unroll
@@ -462,8 +497,8 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
     for (int c = 0; c < 8; ++c) {
         bf16x8 x[TT][3];
         split_tiles<TT>(h, c, x);
-        if (N.mto == 2) split_chunk<TT, 2, true>(buf + c * 2 * 3072, x, acc, lo);
-        else split_chunk<TT, 1, true>(buf + c * 3072, x, acc, lo);
+        if (N.mto == 2) split_chunk<TT, 2, true>(buf + c * 2 * 3072, x, acc, lo, sg);
+        else split_chunk<TT, 1, true>(buf + c * 3072, x, acc, lo, sg);
     }
 #pragma unroll
     for (int t = 0; t < TT; ++t) {
@@ -532,6 +567,8 @@ __global__ void __launch_bounds__(SPLIT ? wide::kSplitWaves * 64 : wide::kThread
     sg.idx = -1;
     sg.cur = -1;
     sg.bytes = SBYTES;
+    sg.blob = a.blob;
+    sg.psrc = sg.pdst = sg.pnext = sg.pend = 0;
     for (int q = 0; q < kWideBufs - 1 && q < sg.n; ++q) dma<NW>(a, cref(sg.sched + q), sg.slot(q));
 
     for (int i = tid; i < a.tab_ints; i += NT) tab[i] = a.tables[i];
