@@ -228,7 +228,7 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
         }
         if (P.wsplit) {
             c->wstab_bytes = ((int)P.wstables.size() * 4 + 15) / 16 * 16;
-            c->wslds = (size_t)df::kWideBufs * df::kWideSplitStageBytes + c->wstab_bytes +
+            c->wslds = (size_t)df::kWideSplitBufs * df::kWideSplitStageBytes + c->wstab_bytes +
                        (size_t)df::kWideWaves * 16 * df::kWideT * P.stride * 4;
             if (c->wslds > 160 * 1024) {
                 df_chain_destroy(c);

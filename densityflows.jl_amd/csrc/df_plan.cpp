@@ -457,7 +457,8 @@ void build_wide_split(const df_chain_desc* desc, Plan& P) {
         for (int k = 0; k < 32 * nc0; ++k) P.wstables.push_back(k < L.n_nn ? L.axis_nn[k] - 1 : zero_slot);
         auto pack = [&](const df_dense_desc* net, int d0, WNet& N) {
             N.stage0 = (int)P.wsstages.size();
-            N.nst0 = nc0;
+            N.nst0 = nc0 * kWideSplitHalves;
+            N.nso = (kWideSplitHalves == 2 && N.mto == 2) ? 2 : 1;
             auto new_stage = [&](int bytes) -> int64_t {
                 DevStage st{};
                 st.src_off = (int64_t)P.wsblob.size();
@@ -485,10 +486,18 @@ void build_wide_split(const df_chain_desc* desc, Plan& P) {
                                 std::memcpy(&P.wsblob[at], &h, 2);
                             }
             };
-            for (int c = 0; c < nc0; ++c) chunk(new_stage(kWideSplitStageBytes), 0, c, 16, true);
-            for (int c = 0; c < 8; ++c) chunk(new_stage(kWideSplitStageBytes), 1, c, 16, false);
-            const int64_t ob = new_stage(8 * N.mto * 3 * 1024);
-            for (int c = 0; c < 8; ++c) chunk(ob + (int64_t)c * N.mto * 3 * 1024, 2, c, N.mto, false);
+            constexpr int MH = 16 / kWideSplitHalves;  // m-tiles per stage
+            for (int c = 0; c < nc0; ++c)
+                for (int hv = 0; hv < kWideSplitHalves; ++hv)
+                    chunk(new_stage(kWideSplitStageBytes), 0, c, MH, true, MH * hv);
+            for (int c = 0; c < 8; ++c)
+                for (int hv = 0; hv < kWideSplitHalves; ++hv)
+                    chunk(new_stage(kWideSplitStageBytes), 1, c, MH, false, MH * hv);
+            const int cps = 8 / N.nso;  // output chunks per stage
+            for (int so = 0; so < N.nso; ++so) {
+                const int64_t ob = new_stage(cps * N.mto * 3 * 1024);
+                for (int c = 0; c < cps; ++c) chunk(ob + (int64_t)c * N.mto * 3 * 1024, 2, so * cps + c, N.mto, false);
+            }
             P.split_flops_per_sample += 2.0 * ((double)net[0].in_dim * net[0].out_dim +
                                                (double)net[1].in_dim * net[1].out_dim +
                                                (double)net[2].in_dim * net[2].out_dim);
@@ -499,7 +508,7 @@ void build_wide_split(const df_chain_desc* desc, Plan& P) {
     auto sched = [&](bool fwd) {
         std::vector<int32_t> out;
         auto net = [&](const WNet& N) {
-            for (int s = 0; s < N.nst0 + 9; ++s) out.push_back(N.stage0 + s);
+            for (int s = 0; s < N.nst0 + 8 * kWideSplitHalves + N.nso; ++s) out.push_back(N.stage0 + s);
         };
         for (int it = 0; it < P.n_layers; ++it) {
             const WLayer& L = P.wslayers[fwd ? it : P.n_layers - 1 - it];

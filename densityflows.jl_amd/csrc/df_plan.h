@@ -120,11 +120,19 @@ constexpr int kWideStageBytes = 32 * 1024;
 constexpr int kWideBufs = DF_WIDE_NB;   // LDS stage ring: the DMA runs kWideBufs − 1 stages ahead
 constexpr int kWideWaves = 4;     // one wave per SIMD (512 registers each)
 constexpr int kWideT = 2;         // 16-sample tiles per wave held in registers (3 spills)
-constexpr int kWideSplitStageBytes = 48 * 1024;  // SPLIT: one 32-input chunk of 16 m-tiles × 3 planes
+#ifndef DF_WSPLIT_HALF
+#define DF_WSPLIT_HALF 0
+#endif
+// SPLIT stages: half a 32-input chunk (8 m-tiles × 3 planes, 24 KiB) in a 4-slot ring
+// (the DMA three stages ahead), or (DF_WSPLIT_HALF=0) a whole chunk in a 2-slot ring
+constexpr int kWideSplitHalves = DF_WSPLIT_HALF ? 2 : 1;
+constexpr int kWideSplitStageBytes = 48 * 1024 / kWideSplitHalves;
+constexpr int kWideSplitBufs = DF_WSPLIT_HALF ? 4 : 2;
 
 struct WNet {
     int32_t stage0;   // first stage id (wide blob)
-    int32_t nst0;     // stages of the first Dense (1 or 2)
+    int32_t nst0;     // stages of the first Dense (1 or 2; SPLIT: chunks × kWideSplitHalves)
+    int32_t nso;      // SPLIT: stages of the output Dense (1, or 2 when half stages split mto = 2)
     int32_t ks;       // first-Dense k-steps (ceil(in/4))
     int32_t n_out, mto;
     int32_t act0, act1, act_out;

@@ -61,6 +61,7 @@ struct WStager {
     int idx;
     int cur;
     int bytes;  // ring slot size: kWideStageBytes, or kWideSplitStageBytes (SPLIT)
+    int nb;     // ring slots: kWideBufs, or kWideSplitBufs (SPLIT)
     // staggered DMA (SPLIT): this wave's pieces of the next stage, issued one per
     // m-tile by split_chunk instead of all at the stage switch
     const uint8_t* blob;
@@ -68,7 +69,7 @@ struct WStager {
     int pdst;   // its ring slot's byte offset from base
     int pnext, pend;
     __device__ __forceinline__ uint8_t* buf() const { return slot(idx); }
-    __device__ __forceinline__ uint8_t* slot(int i) const { return base + (i % kWideBufs) * bytes; }
+    __device__ __forceinline__ uint8_t* slot(int i) const { return base + (i % nb) * bytes; }
     template <int NW>
     __device__ __forceinline__ void issue_one() {
         if (pnext < pend) {
@@ -104,7 +105,15 @@ __device__ __forceinline__ void wait_vmcnt(int k) {
         case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
         case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
         case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+        case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+        case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
     }
 }
 
@@ -124,15 +133,15 @@ __device__ __forceinline__ void dma(const ChainArgs& a, int s, uint8_t* dst) {
 // Vector-memory loads return in order, so waiting until at most the newer
 // in-flight stages' DMA instructions of this wave are outstanding means this
 // wave's part of stage s has landed; the barrier then covers every wave's part.
-template <int NW = kWideWaves, bool STAGGER = false>
+template <int NW = kWideWaves, bool STAGGER = false, int NB = kWideBufs>
 __device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
     if (s == sg.cur) return;
-    if (STAGGER) sg.issue_all<NW>();  // pieces of stage s not issued yet
+    if (STAGGER) sg.issue_all<NW>();  // pending pieces (of the newest stage in flight) not issued yet
     const int nidx = sg.idx + 1;
-    if (kWideBufs > 2) {
+    if (NB > 2) {  // the NB − 2 newer stages' pieces may stay in flight (issued in order after stage s's)
         const int wave = threadIdx.x >> 6;
         int newer = 0;
-        for (int q = 1; q < kWideBufs - 1; ++q)
+        for (int q = 1; q < NB - 1; ++q)
             if (nidx + q < sg.n) newer += dma_ops<NW>(cref(a.stages + cref(sg.sched + nidx + q)).bytes, wave);
         wait_vmcnt(newer);
     } else {
@@ -155,15 +164,15 @@ __device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
         sg.n = 0;
         return;
     }
-    if (nidx + kWideBufs - 1 < sg.n) {
+    if (nidx + NB - 1 < sg.n) {
         if (STAGGER) {
-            const DevStage& st = cref(a.stages + cref(sg.sched + nidx + kWideBufs - 1));
+            const DevStage& st = cref(a.stages + cref(sg.sched + nidx + NB - 1));
             sg.psrc = (int)st.src_off;
-            sg.pdst = (int)(sg.slot(nidx + kWideBufs - 1) - sg.base);
+            sg.pdst = (int)(sg.slot(nidx + NB - 1) - sg.base);
             sg.pnext = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
             sg.pend = st.bytes >> 10;
         } else {
-            dma<NW>(a, cref(sg.sched + nidx + kWideBufs - 1), sg.slot(nidx + kWideBufs - 1));
+            dma<NW>(a, cref(sg.sched + nidx + NB - 1), sg.slot(nidx + NB - 1));
         }
     }
 }
@@ -339,6 +348,9 @@ constexpr int kSplitT = 8 / DF_WSPLIT_WAVES;        // 128 samples per workgroup
 #ifndef DF_WIDE_STAGGER
 #define DF_WIDE_STAGGER 1
 #endif
+#ifndef DF_WIDE_PF
+#define DF_WIDE_PF 1
+#endif
 
 // acc += W·x over one 32-input chunk for m-tiles [0, MT): planes [m][p][lane][8] at
 // buf (lane offset applied), activation planes x[t][p]; the next m-tile's planes
@@ -352,32 +364,38 @@ constexpr int kSplitT = 8 / DF_WSPLIT_WAVES;        // 128 samples per workgroup
 //   the total takes one per chunk and lo's are relative to the small terms.  hi
 //   and lo are touched only by MFMAs (AGPR-resident); the caller adds them once.
 //   !HILO (the one- or two-chunk first Dense): all six products onto hi.
-template <int TT, int MT, bool HILO, int MA>
+template <int TT, int MT, bool HILO, int MA, int M0 = 0>
 __device__ __forceinline__ void split_chunk(const uint8_t* buf, const bf16x8 (&x)[TT][3], f32x4 (&hi)[TT][MA],
                                             f32x4 (&lo)[TT][MA], WStager& sg) {
-    bf16x8 w[2][3];
+    // fragment ring, DF_WIDE_PF m-tiles ahead
+    constexpr int PF = DF_WIDE_PF;
+    bf16x8 w[PF + 1][3];
 #pragma unroll
-    for (int p = 0; p < 3; ++p) w[0][p] = *reinterpret_cast<const bf16x8*>(buf + p * 1024);
+    for (int q = 0; q < PF; ++q)
+        if (q < MT)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) w[q][p] = *reinterpret_cast<const bf16x8*>(buf + q * 3072 + p * 1024);
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-        const int cb = m & 1;
-        if (m + 1 < MT) {
+        const int cb = m % (PF + 1);
+        if (m + PF < MT) {
 #pragma unroll
-            for (int p = 0; p < 3; ++p) w[cb ^ 1][p] = *reinterpret_cast<const bf16x8*>(buf + (m + 1) * 3072 + p * 1024);
+            for (int p = 0; p < 3; ++p)
+                w[(m + PF) % (PF + 1)][p] = *reinterpret_cast<const bf16x8*>(buf + (m + PF) * 3072 + p * 1024);
         }
 #pragma unroll
         for (int t = 0; t < TT; ++t) {
-            f32x4 v = HILO ? lo[t][m] : hi[t][m];
+            f32x4 v = HILO ? lo[t][M0 + m] : hi[t][M0 + m];
             v = mfma_bf(w[cb][2], x[t][0], v);
             v = mfma_bf(w[cb][1], x[t][1], v);
             v = mfma_bf(w[cb][0], x[t][2], v);
             v = mfma_bf(w[cb][1], x[t][0], v);
             v = mfma_bf(w[cb][0], x[t][1], v);
             if (HILO) {
-                lo[t][m] = v;
-                hi[t][m] = mfma_bf(w[cb][0], x[t][0], hi[t][m]);
+                lo[t][M0 + m] = v;
+                hi[t][M0 + m] = mfma_bf(w[cb][0], x[t][0], hi[t][M0 + m]);
             } else {
-                hi[t][m] = mfma_bf(w[cb][0], x[t][0], v);
+                hi[t][M0 + m] = mfma_bf(w[cb][0], x[t][0], v);
             }
         }
         if (DF_WIDE_STAGGER) sg.issue_one<kSplitWaves>();  // one DMA piece of the next stage per m-tile
@@ -418,8 +436,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-        if (c < N.nst0) {
-            ensure<kSplitWaves, DF_WIDE_STAGGER != 0>(N.stage0 + c, sg, a);
+        if (kWideSplitHalves * c < N.nst0) {
             bf16x8 x[TT][3];
 #pragma unroll
             for (int t = 0; t < TT; ++t) {
@@ -428,7 +445,12 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
                 for (int e = 0; e < 8; ++e) v[e] = state[ro[t] + sfeat[32 * c + 8 * g + e]];
                 split8(v, x[t][0], x[t][1], x[t][2]);
             }
-            split_chunk<TT, 16, false>(sg.buf() + lane * 16, x, acc, acc, sg);
+            ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(N.stage0 + kWideSplitHalves * c, sg, a);
+            split_chunk<TT, 16 / kWideSplitHalves, false, 16, 0>(sg.buf() + lane * 16, x, acc, acc, sg);
+            if constexpr (kWideSplitHalves == 2) {
+                ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(N.stage0 + 2 * c + 1, sg, a);
+                split_chunk<TT, 8, false, 16, 8>(sg.buf() + lane * 16, x, acc, acc, sg);
+            }
         }
     }
 #pragma unroll
@@ -450,7 +472,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
     }
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        ensure<kSplitWaves, DF_WIDE_STAGGER != 0>(N.stage0 + N.nst0 + c, sg, a);
+        ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(N.stage0 + N.nst0 + kWideSplitHalves * c, sg, a);
         if (hs && c == 0) {  // training: keep H0 (as in eval_net)
 #pragma unroll
             for (int t = 0; t < TT; ++t)
@@ -461,7 +483,11 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
         }
         bf16x8 x[TT][3];
         split_tiles<TT>(h, c, x);
-        split_chunk<TT, 16, true>(sg.buf() + lane * 16, x, acc, lo, sg);
+        split_chunk<TT, 16 / kWideSplitHalves, true, 16, 0>(sg.buf() + lane * 16, x, acc, lo, sg);
+        if constexpr (kWideSplitHalves == 2) {
+            ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(N.stage0 + N.nst0 + 2 * c + 1, sg, a);
+            split_chunk<TT, 8, true, 16, 8>(sg.buf() + lane * 16, x, acc, lo, sg);
+        }
     }
 #pragma unroll
     for (int t = 0; t < TT; ++t)
@@ -473,7 +499,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
         }
 
     // ---- output Dense (<= 32 outputs) ----
-    ensure<kSplitWaves, DF_WIDE_STAGGER != 0>(N.stage0 + N.nst0 + 8, sg, a);
+    ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(N.stage0 + N.nst0 + 8 * kWideSplitHalves, sg, a);
     if (hs) {  // training: keep H1
         float* hs1 = hs + a.batch * a.hsave_w;
 #pragma unroll
@@ -483,7 +509,6 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
                 for (int m = 0; m < 16; ++m)
                     __builtin_nontemporal_store(h[t][m], reinterpret_cast<f32x4*>(hs1 + gs[t] * a.hsave_w + 16 * m + 4 * g));
     }
-    const uint8_t* buf = sg.buf() + lane * 16;
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
         const f32x4 b = m < N.mto ? bias4(a.wbias + N.bo, m) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -493,11 +518,14 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
             lo[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
     }
+    const int so0 = N.stage0 + N.nst0 + 8 * kWideSplitHalves;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
+        if (N.nso == 2 && c == 4) ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(so0 + 1, sg, a);
+        const uint8_t* buf = sg.buf() + lane * 16;
         bf16x8 x[TT][3];
         split_tiles<TT>(h, c, x);
-        if (N.mto == 2) split_chunk<TT, 2, true>(buf + c * 2 * 3072, x, acc, lo, sg);
+        if (N.mto == 2) split_chunk<TT, 2, true>(buf + (c & (8 / N.nso - 1)) * 2 * 3072, x, acc, lo, sg);
         else split_chunk<TT, 1, true>(buf + c * 3072, x, acc, lo, sg);
     }
 #pragma unroll
@@ -547,7 +575,8 @@ __global__ void __launch_bounds__(SPLIT ? wide::kSplitWaves * 64 : wide::kThread
     constexpr int NT = NW * 64;
 
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int stage_area = kWideBufs * SBYTES;
+    constexpr int NB = SPLIT ? kWideSplitBufs : kWideBufs;  // ring slots
+    const int stage_area = NB * SBYTES;
     int32_t* tab = reinterpret_cast<int32_t*>(smem + stage_area);
     float* state = reinterpret_cast<float*>(smem + stage_area + a.tab_bytes);
 
@@ -567,9 +596,10 @@ __global__ void __launch_bounds__(SPLIT ? wide::kSplitWaves * 64 : wide::kThread
     sg.idx = -1;
     sg.cur = -1;
     sg.bytes = SBYTES;
+    sg.nb = NB;
     sg.blob = a.blob;
     sg.psrc = sg.pdst = sg.pnext = sg.pend = 0;
-    for (int q = 0; q < kWideBufs - 1 && q < sg.n; ++q) dma<NW>(a, cref(sg.sched + q), sg.slot(q));
+    for (int q = 0; q < NB - 1 && q < sg.n; ++q) dma<NW>(a, cref(sg.sched + q), sg.slot(q));
 
     for (int i = tid; i < a.tab_ints; i += NT) tab[i] = a.tables[i];
     for (int i = tid; i < S * d; i += NT) {

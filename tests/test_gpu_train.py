@@ -171,6 +171,28 @@ def test_gradient_parity(cuda, path, name, B):
     assert worst <= 1.0, f"gradient violation ratio {worst}"
 
 
+@pytest.mark.parametrize("name,B", [("cfg2", 3001), ("cfg5", 300), ("wide", 700)])
+def test_gradient_parity_exact_f32(cuda, monkeypatch, name, B):
+    """The exact-f32 MFMA kernels (DF_F32_EXACT=1: no bf16x3 SPLIT anywhere, DESIGN
+    §1b) keep passing the same gradient criterion, and the SPLIT and exact gradients
+    agree to it."""
+    spec, chain, d, n = _setup(name)
+    x, th = _inputs(d, n, B)
+    grads = {}
+    for exact in ("1", "0"):
+        monkeypatch.setenv("DF_F32_EXACT", exact)
+        spec, chain, d, n = _setup(name)   # fresh chain and trainer: the plan reads the env
+        tr = HIPTrainer(chain.hip(), Adam())
+        grads[exact], _ = _gpu_grad(tr, x, th, cuda)
+    loss, ref = O.nll_and_grad(spec, x, th if n else np.zeros((0, B)))
+    ref = _flat_oracle_grads(spec, ref)
+    for sl in _tensor_slices(spec):
+        for exact in ("1", "0"):
+            ok, r = close(grads[exact][sl], ref[sl], G_RTOL, G_ATOL)
+            assert ok, (exact, r)
+        assert close(grads["0"][sl], grads["1"][sl], G_RTOL, G_ATOL)[0]
+
+
 @pytest.mark.parametrize("recompute", [False, True])
 @pytest.mark.parametrize("name,B", [("wide", 700), ("wide", 5), ("cfg5", 300)])
 def test_gradient_parity_layerwise_wide(cuda, monkeypatch, name, B, recompute):
