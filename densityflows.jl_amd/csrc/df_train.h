@@ -25,6 +25,11 @@
 
 namespace df {
 
+#ifndef DF_TRAIN_WAVES
+#define DF_TRAIN_WAVES 8
+#endif
+constexpr int kTrainWaves = DF_TRAIN_WAVES;     // waves per workgroup of the fused net kernel
+constexpr int kTrainThreads = 64 * kTrainWaves;
 constexpr int kTS = 20;  // row stride (floats) of the per-wave transpose buffers [row][16 samples]
 
 namespace trn {

@@ -124,7 +124,7 @@ unsigned blocks_for(int64_t count, int threads) { return (unsigned)((count + thr
 }  // namespace
 
 size_t train_net_lds(int ht, const GNet& g) {
-    const size_t tarea = (size_t)kWavesPerBlock * 2 * 16 * ht * kTS * 4;
+    const size_t tarea = (size_t)kTrainWaves * 2 * 16 * ht * kTS * 4;
     const size_t red = (size_t)g.p_count * 4;
     if (g.split) return (size_t)g.sfwd_bytes + ht * 1024 + g.st_bytes + (tarea > red ? tarea : red);
     return (size_t)g.fwd_bytes + g.t_bytes + (tarea > red ? tarea : red);
@@ -151,13 +151,13 @@ hipError_t launch_train_net(int ht, int nh, int am, const TrainArgs& a, unsigned
     void* k = train_ptr(ht, nh, am, a.net.split != 0);
     if (!k) return hipErrorInvalidValue;
     void* args[] = {const_cast<TrainArgs*>(&a)};
-    return hipLaunchKernel(k, dim3(grid), dim3(kBlockThreads), args, lds, st);
+    return hipLaunchKernel(k, dim3(grid), dim3(kTrainThreads), args, lds, st);
 }
 
 hipError_t train_net_occupancy(int ht, int nh, int am, size_t lds, int* blocks, bool split) {
     void* k = train_ptr(ht, nh, am, split);
     if (!k) return hipErrorInvalidValue;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k, kBlockThreads, lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k, kTrainThreads, lds);
 }
 
 hipError_t launch_scale(float* dst, const float* src, float s, int64_t count, hipStream_t st) {

@@ -994,7 +994,7 @@ int df_train_gradient(df_train* t, const float* x, const float* theta_raw, int64
         return e == hipSuccess ? DF_OK : hip_err(e, "gradient reduction launch");
     }
     const int64_t ntiles = (batch + 15) / 16;
-    const int grid = (int)std::min<int64_t>(t->grid, (ntiles + kWavesPerBlock - 1) / kWavesPerBlock);
+    const int grid = (int)std::min<int64_t>(t->grid, (ntiles + kTrainWaves - 1) / kTrainWaves);
     for (const SweepOp& op : t->ops) {
         const DevLayer& L = P.layers[op.layer];
         if (op.net < 0) {

@@ -124,7 +124,7 @@ __device__ __forceinline__ uni::bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
 }
 
 template <int HT, int NH, int AM, bool SPLIT = false>
-__global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a) {
+__global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a) {
     using namespace trn;
     constexpr bool RELU = (AM == AM_RELU);
     constexpr bool PRE = (AM == AM_PRE);
@@ -151,12 +151,12 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
 
     {  // the net's forward and transposed fragments → LDS
         const f32x4* src = reinterpret_cast<const f32x4*>(SPLIT ? a.sblob + G.sfwd_src : a.blob + G.fwd_src);
-        for (int i = tid; i < fwd_bytes / 16; i += kBlockThreads) reinterpret_cast<f32x4*>(fw)[i] = src[i];
+        for (int i = tid; i < fwd_bytes / 16; i += kTrainThreads) reinterpret_cast<f32x4*>(fw)[i] = src[i];
         const f32x4* srt = reinterpret_cast<const f32x4*>(a.tblob + G.t_src);
-        for (int i = tid; i < t_bytes / 16; i += kBlockThreads) reinterpret_cast<f32x4*>(tw)[i] = srt[i];
+        for (int i = tid; i < t_bytes / 16; i += kTrainThreads) reinterpret_cast<f32x4*>(tw)[i] = srt[i];
         if constexpr (SPLIT) {
             const f32x4* sst = reinterpret_cast<const f32x4*>(a.tsblob + G.st_src);
-            for (int i = tid; i < G.st_bytes / 16; i += kBlockThreads) reinterpret_cast<f32x4*>(stw)[i] = sst[i];
+            for (int i = tid; i < G.st_bytes / 16; i += kTrainThreads) reinterpret_cast<f32x4*>(stw)[i] = sst[i];
         }
     }
     // zero rows of the δ_out transpose that no lane writes (rows >= 4)
@@ -237,8 +237,8 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
     };
 
     const int64_t ntiles = (a.batch + 15) / 16;
-    const int64_t tstride = (int64_t)gridDim.x * kWavesPerBlock;
-    for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wave; tile < ntiles; tile += tstride) {
+    const int64_t tstride = (int64_t)gridDim.x * kTrainWaves;
+    for (int64_t tile = (int64_t)blockIdx.x * kTrainWaves + wave; tile < ntiles; tile += tstride) {
         const int64_t s = tile * 16 + j;
         const bool valid = s < a.batch;
         zxl = zxp8;
@@ -475,7 +475,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
     // ---- workgroup reduction (fixed wave order) → partial[blockIdx.x] ----
     __syncthreads();
     float* R = tarea;
-    for (int i = tid; i < G.p_count; i += kBlockThreads) R[i] = 0.f;
+    for (int i = tid; i < G.p_count; i += kTrainThreads) R[i] = 0.f;
 #pragma unroll
     for (int m = 0; m < HT; ++m) gb0[m] = uni::xgroup_sum(gb0[m]);
 #pragma unroll
@@ -486,7 +486,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
     const int wo0 = G.w_off[0] - G.p_begin, bo0 = G.b_off[0] - G.p_begin;
     const int wo1 = G.w_off[1] - G.p_begin, bo1 = G.b_off[1] - G.p_begin;
     const int wo2 = G.w_off[2] - G.p_begin, bo2 = G.b_off[2] - G.p_begin;
-    for (int w = 0; w < kWavesPerBlock; ++w) {
+    for (int w = 0; w < kTrainWaves; ++w) {
         if (wave == w) {
 #pragma unroll
             for (int m = 0; m < HT; ++m)
@@ -523,7 +523,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) train_net_kernel(TrainArgs a
         __syncthreads();
     }
     float* dst = a.partial + (int64_t)blockIdx.x * a.p_total + G.p_begin;
-    for (int i = tid; i < G.p_count; i += kBlockThreads) dst[i] = R[i];
+    for (int i = tid; i < G.p_count; i += kTrainThreads) dst[i] = R[i];
 }
 
 template <int HT, int NH, int AM, bool SPLIT = false>
