@@ -420,6 +420,26 @@ __device__ __forceinline__ void split_tiles(const f32x4 (&h)[TT][16], int c, bf1
 //                features 32c + 8g + e
 //   hidden Dense 8 stages [m < 16][p][lane][8], one 32-input chunk each (hi/lo)
 //   output Dense one stage [c < 8][m < mto][p][lane][8] (hi/lo)
+#ifndef DF_WSNAP_SPREAD
+#define DF_WSNAP_SPREAD 1
+#endif
+// Training snapshot of a hidden activation (H0 or H1, rows of sample gs[t]) during
+// 32-input chunk c of the Dense that consumes it. SPREAD: the chunk's own two m-tiles
+// (its stores drain during the chunk's MFMAs; a stage switch waits vmcnt(0), so a
+// 16-tile burst would stall the next one), else all 16 tiles at chunk 0.
+template <int TT, bool SPREAD>
+__device__ __forceinline__ void snapshot(const f32x4 (&h)[TT][16], float* dst, const int64_t (&gs)[TT], int w, int c) {
+    const int g = (threadIdx.x & 63) >> 4;
+    if (!SPREAD && c != 0) return;
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+        if (gs[t] >= 0)
+#pragma unroll
+            for (int m = 0; m < 16; ++m)
+                if (!SPREAD || (m >> 1) == c)
+                    __builtin_nontemporal_store(h[t][m], reinterpret_cast<f32x4*>(dst + gs[t] * w + 16 * m + 4 * g));
+}
+
 template <int TT>
 __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N, const int32_t* sfeat,
                                                const float* state, const int (&ro)[TT], WStager& sg,
@@ -473,16 +493,9 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(N.stage0 + N.nst0 + kWideSplitHalves * c, sg, a);
-        if (hs && c == 0) {  // training: keep H0 (as in eval_net)
-#pragma unroll
-            for (int t = 0; t < TT; ++t)
-                if (gs[t] >= 0)
-#pragma unroll
-                    for (int m = 0; m < 16; ++m)
-                        __builtin_nontemporal_store(h[t][m], reinterpret_cast<f32x4*>(hs + gs[t] * a.hsave_w + 16 * m + 4 * g));
-        }
         bf16x8 x[TT][3];
         split_tiles<TT>(h, c, x);
+        if (hs) snapshot<TT, DF_WSNAP_SPREAD != 0>(h, hs, gs, a.hsave_w, c);  // training: keep H0 (as in eval_net)
         split_chunk<TT, 16 / kWideSplitHalves, true, 16, 0>(sg.buf() + lane * 16, x, acc, lo, sg);
         if constexpr (kWideSplitHalves == 2) {
             ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(N.stage0 + N.nst0 + 2 * c + 1, sg, a);
@@ -500,15 +513,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
 
     // ---- output Dense (<= 32 outputs) ----
     ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(N.stage0 + N.nst0 + 8 * kWideSplitHalves, sg, a);
-    if (hs) {  // training: keep H1
-        float* hs1 = hs + a.batch * a.hsave_w;
-#pragma unroll
-        for (int t = 0; t < TT; ++t)
-            if (gs[t] >= 0)
-#pragma unroll
-                for (int m = 0; m < 16; ++m)
-                    __builtin_nontemporal_store(h[t][m], reinterpret_cast<f32x4*>(hs1 + gs[t] * a.hsave_w + 16 * m + 4 * g));
-    }
+    float* const hs1 = hs ? hs + a.batch * a.hsave_w : nullptr;  // training: keep H1
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
         const f32x4 b = m < N.mto ? bias4(a.wbias + N.bo, m) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -525,6 +530,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
         const uint8_t* buf = sg.buf() + lane * 16;
         bf16x8 x[TT][3];
         split_tiles<TT>(h, c, x);
+        if (hs1) snapshot<TT, DF_WSNAP_SPREAD != 0>(h, hs1, gs, a.hsave_w, c);
         if (N.mto == 2) split_chunk<TT, 2, true>(buf + (c & (8 / N.nso - 1)) * 2 * 3072, x, acc, lo, sg);
         else split_chunk<TT, 1, true>(buf + c * 3072, x, acc, lo, sg);
     }
