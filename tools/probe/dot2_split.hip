@@ -1,0 +1,70 @@
+// Probe: is v_dot2c_f32_bf16(h, {-1, 0}, x) == x - (float)h bitwise on gfx950, where
+// h = RNE bf16 pair of (x0, x1)?  (The SPLIT kernels' remainder r = x - hi without
+// the two bf16 → f32 unpacks.)  Checks both remainder levels of the bf16x3 split over
+// 2^24 values per pass: random magnitudes over the normal f32 range, relu outputs,
+// values near bf16 ties, tiny values near the denormal range.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <cstring>
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t hash(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+
+__global__ void k(uint32_t seed, int pass, unsigned long long* bad, uint32_t* example) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t u0 = hash(i * 2 + seed), u1 = hash(i * 2 + 1 + seed * 7919u);
+    if (pass == 1) { u0 = (u0 & 0x807fffffu) | (((u0 >> 23) % 40 + 107) << 23); u1 = (u1 & 0x807fffffu) | (((u1 >> 23) % 40 + 107) << 23); }
+    if (pass == 2) { u0 = (u0 & 0x807f0000u) | 0x8000u | (120u << 23); u1 = (u1 & 0xff7fffffu); }  // bf16 ties
+    if (pass == 3) { u0 = (u0 & 0x807fffffu) | ((1 + (u0 >> 23) % 30) << 23); u1 = (u1 & 0x807fffffu) | ((1 + (u1 >> 23) % 30) << 23); }
+    float x0 = __uint_as_float(u0), x1 = __uint_as_float(u1);
+    if ((u0 & 0x7f800000u) == 0x7f800000u || (u1 & 0x7f800000u) == 0x7f800000u) return;  // inf / nan
+    if (pass == 1) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+    const bf16x2 n0 = {(__bf16)-1.0f, (__bf16)0.0f};
+    const bf16x2 n1 = {(__bf16)0.0f, (__bf16)-1.0f};
+    const bf16x2 h = {(__bf16)x0, (__bf16)x1};
+    const float r0 = x0 - (float)h[0], r1 = x1 - (float)h[1];
+    const float d0 = __builtin_amdgcn_fdot2_f32_bf16(h, n0, x0, false);
+    const float d1 = __builtin_amdgcn_fdot2_f32_bf16(h, n1, x1, false);
+    const bf16x2 m = {(__bf16)r0, (__bf16)r1};
+    const float l0 = r0 - (float)m[0], l1 = r1 - (float)m[1];
+    const float e0 = __builtin_amdgcn_fdot2_f32_bf16(m, n0, r0, false);
+    const float e1 = __builtin_amdgcn_fdot2_f32_bf16(m, n1, r1, false);
+    const bool ok = __float_as_uint(d0) == __float_as_uint(r0) && __float_as_uint(d1) == __float_as_uint(r1) &&
+                    __float_as_uint(e0) == __float_as_uint(l0) && __float_as_uint(e1) == __float_as_uint(l1);
+    if (!ok) {
+        if (atomicAdd(bad, 1ull) == 0) {
+            example[0] = u0; example[1] = u1;
+            example[2] = __float_as_uint(r0); example[3] = __float_as_uint(d0);
+            example[4] = __float_as_uint(l0); example[5] = __float_as_uint(e0);
+        }
+    }
+}
+
+int main() {
+    unsigned long long* bad;
+    uint32_t* ex;
+    hipMalloc(&bad, 8);
+    hipMalloc(&ex, 32);
+    int rc = 0;
+    const char* names[] = {"random normal f32", "relu outputs 2^-20..2^20", "bf16 ties", "near-denormal"};
+    for (int pass = 0; pass < 4; ++pass) {
+        unsigned long long nb = 0;
+        uint32_t e[6] = {0, 0, 0, 0, 0, 0};
+        hipMemset(bad, 0, 8);
+        hipMemset(ex, 0, 32);
+        hipLaunchKernelGGL(k, dim3(1 << 16), dim3(256), 0, 0, 1234u + pass, pass, bad, ex);
+        hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
+        hipMemcpy(e, ex, 24, hipMemcpyDeviceToHost);
+        printf("%-28s mismatches %llu of 2^24", names[pass], nb);
+        if (nb) printf("  e.g. x0=%08x x1=%08x r0=%08x dot=%08x l0=%08x dot=%08x", e[0], e[1], e[2], e[3], e[4], e[5]);
+        printf("\n");
+        if (nb && pass < 3) rc = 1;
+    }
+    hipFree(bad);
+    hipFree(ex);
+    return rc;
+}
