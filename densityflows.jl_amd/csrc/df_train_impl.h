@@ -109,13 +109,12 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void split4(f32x4 v, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const __bf16 h = (__bf16)v[e];
-        const float r = v[e] - (float)h;
-        const __bf16 m = (__bf16)r;
-        p0[e] = h;
-        p1[e] = m;
-        p2[e] = (__bf16)(r - (float)m);
+    for (int e = 0; e < 4; e += 2) {
+        uni::bf16x2 h, m, l;
+        uni::split2(v[e], v[e + 1], h, m, l);
+        p0[e] = h[0]; p0[e + 1] = h[1];
+        p1[e] = m[0]; p1[e + 1] = m[1];
+        p2[e] = l[0]; p2[e + 1] = l[1];
     }
 }
 

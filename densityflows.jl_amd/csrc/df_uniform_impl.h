@@ -381,16 +381,46 @@ __device__ __forceinline__ f32x4 mfma_bf(const bf16x8& a, const bf16x8& b, f32x4
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// Remainder x - (float)h[S] of an RNE bf16 pair h, as one v_dot2c_f32_bf16
+// (x + h·(-1, 0) or x + h·(0, -1)): the difference is exactly representable, and the
+// dot2 returns it bitwise (tools/probe/dot2_split.hip), so the two bf16 → f32 unpacks
+// and the f32 subtract of the plain form become one instruction per value.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+#ifndef DF_SPLIT_DOT2
+#define DF_SPLIT_DOT2 1
+#endif
+template <int S>
+__device__ __forceinline__ float split_rem(bf16x2 h, float x) {
+#if DF_SPLIT_DOT2
+    // (-1, 0) is materialised by a v_mov: the compiler would otherwise encode it as the
+    // inline constant -1.0, which the hardware reads as the f32 0xbf800000, i.e. (0, -1)
+    // (probe: tools/probe/dot2_split.hip).  The asm is pure, so it is hoisted and shared.
+    uint32_t c;
+    if (S == 0) asm("v_mov_b32 %0, 0xbf80" : "=v"(c));
+    else c = 0xbf800000u;
+    return __builtin_amdgcn_fdot2_f32_bf16(h, __builtin_bit_cast(bf16x2, c), x, false);
+#else
+    return x - (float)h[S];
+#endif
+}
+
+// 2 f32 values → their three bf16 planes (pairs).
+__device__ __forceinline__ void split2(float a, float b, bf16x2& p0, bf16x2& p1, bf16x2& p2) {
+    p0 = bf16x2{(__bf16)a, (__bf16)b};
+    const float ra = split_rem<0>(p0, a), rb = split_rem<1>(p0, b);
+    p1 = bf16x2{(__bf16)ra, (__bf16)rb};
+    p2 = bf16x2{(__bf16)split_rem<0>(p1, ra), (__bf16)split_rem<1>(p1, rb)};
+}
+
 // 8 f32 values → their three bf16 planes.
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const __bf16 h = (__bf16)v[e];
-        const float r = v[e] - (float)h;
-        const __bf16 m = (__bf16)r;
-        p0[e] = h;
-        p1[e] = m;
-        p2[e] = (__bf16)(r - (float)m);
+    for (int e = 0; e < 8; e += 2) {
+        bf16x2 h, m, l;
+        split2(v[e], v[e + 1], h, m, l);
+        p0[e] = h[0]; p0[e + 1] = h[1];
+        p1[e] = m[0]; p1[e + 1] = m[1];
+        p2[e] = l[0]; p2[e + 1] = l[1];
     }
 }
 
@@ -404,13 +434,10 @@ __device__ __forceinline__ void dense_first_split(const uint8_t* buf, const UNet
     bf16x8 b[TT];
 #pragma unroll
     for (int t = 0; t < TT; ++t) {
-        const float x = xin[t][0];
-        const __bf16 h = (__bf16)x;
-        const float r = x - (float)h;
-        const __bf16 m = (__bf16)r;
-        const __bf16 l = (__bf16)(r - (float)m);
+        bf16x2 h, m, l;
+        split2(xin[t][0], 0.f, h, m, l);
         const __bf16 z = (__bf16)0.f;
-        b[t] = bf16x8{h, m, h, l, m, h, z, z};
+        b[t] = bf16x8{h[0], m[0], h[0], l[0], m[0], h[0], z, z};
     }
     const uint8_t* wb = buf + N.off_w0 + lane * 16;
 #pragma unroll

@@ -14,6 +14,7 @@ __device__ __forceinline__ uint32_t hash(uint32_t x) {
     return x;
 }
 
+template <int OPAQUE>
 __global__ void k(uint32_t seed, int pass, unsigned long long* bad, uint32_t* example) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t u0 = hash(i * 2 + seed), u1 = hash(i * 2 + 1 + seed * 7919u);
@@ -21,10 +22,18 @@ __global__ void k(uint32_t seed, int pass, unsigned long long* bad, uint32_t* ex
     if (pass == 2) { u0 = (u0 & 0x807f0000u) | 0x8000u | (120u << 23); u1 = (u1 & 0xff7fffffu); }  // bf16 ties
     if (pass == 3) { u0 = (u0 & 0x807fffffu) | ((1 + (u0 >> 23) % 30) << 23); u1 = (u1 & 0x807fffffu) | ((1 + (u1 >> 23) % 30) << 23); }
     float x0 = __uint_as_float(u0), x1 = __uint_as_float(u1);
-    if ((u0 & 0x7f800000u) == 0x7f800000u || (u1 & 0x7f800000u) == 0x7f800000u) return;  // inf / nan
+    // inf / nan, and |x| that rounds to a bf16 inf (≥ 0x7f7f8000): the pair's other
+    // product is then 0·inf = NaN (activations of that size have overflowed already)
+    if ((u0 & 0x7fffffffu) >= 0x7f7f8000u || (u1 & 0x7fffffffu) >= 0x7f7f8000u) return;
     if (pass == 1) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
-    const bf16x2 n0 = {(__bf16)-1.0f, (__bf16)0.0f};
-    const bf16x2 n1 = {(__bf16)0.0f, (__bf16)-1.0f};
+    bf16x2 n0 = {(__bf16)-1.0f, (__bf16)0.0f};
+    bf16x2 n1 = {(__bf16)0.0f, (__bf16)-1.0f};
+    if (OPAQUE) {  // the constants through VGPRs (no inline-constant encoding)
+        uint32_t c0 = 0x0000bf80u, c1 = 0xbf800000u;
+        asm volatile("" : "+v"(c0), "+v"(c1));
+        n0 = __builtin_bit_cast(bf16x2, c0);
+        n1 = __builtin_bit_cast(bf16x2, c1);
+    }
     const bf16x2 h = {(__bf16)x0, (__bf16)x1};
     const float r0 = x0 - (float)h[0], r1 = x1 - (float)h[1];
     const float d0 = __builtin_amdgcn_fdot2_f32_bf16(h, n0, x0, false);
@@ -51,18 +60,20 @@ int main() {
     hipMalloc(&ex, 32);
     int rc = 0;
     const char* names[] = {"random normal f32", "relu outputs 2^-20..2^20", "bf16 ties", "near-denormal"};
+    for (int opq = 0; opq < 2; ++opq)
     for (int pass = 0; pass < 4; ++pass) {
         unsigned long long nb = 0;
         uint32_t e[6] = {0, 0, 0, 0, 0, 0};
         hipMemset(bad, 0, 8);
         hipMemset(ex, 0, 32);
-        hipLaunchKernelGGL(k, dim3(1 << 16), dim3(256), 0, 0, 1234u + pass, pass, bad, ex);
+        if (opq) hipLaunchKernelGGL(k<1>, dim3(1 << 16), dim3(256), 0, 0, 1234u + pass, pass, bad, ex);
+        else hipLaunchKernelGGL(k<0>, dim3(1 << 16), dim3(256), 0, 0, 1234u + pass, pass, bad, ex);
         hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
         hipMemcpy(e, ex, 24, hipMemcpyDeviceToHost);
-        printf("%-28s mismatches %llu of 2^24", names[pass], nb);
+        printf("%s %-28s mismatches %llu of 2^24", opq ? "vgpr-const  " : "inline-const", names[pass], nb);
         if (nb) printf("  e.g. x0=%08x x1=%08x r0=%08x dot=%08x l0=%08x dot=%08x", e[0], e[1], e[2], e[3], e[4], e[5]);
         printf("\n");
-        if (nb && pass < 3) rc = 1;
+        if (nb && pass < 3 && opq) rc = 1;
     }
     hipFree(bad);
     hipFree(ex);
