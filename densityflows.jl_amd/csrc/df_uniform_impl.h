@@ -432,12 +432,13 @@ __device__ __forceinline__ void dense_first_split(const uint8_t* buf, const UNet
                                                   f32x4 (&acc)[TT][HT]) {
     const int lane = threadIdx.x & 63;
     bf16x8 b[TT];
+    const __bf16 z = (__bf16)0.f;
 #pragma unroll
-    for (int t = 0; t < TT; ++t) {
+    for (int t = 0; t < TT; t += 2) {  // tiles in pairs: one split of two values
         bf16x2 h, m, l;
-        split2(xin[t][0], 0.f, h, m, l);
-        const __bf16 z = (__bf16)0.f;
+        split2(xin[t][0], t + 1 < TT ? xin[t + 1][0] : 0.f, h, m, l);
         b[t] = bf16x8{h[0], m[0], h[0], l[0], m[0], h[0], z, z};
+        if (t + 1 < TT) b[t + 1] = bf16x8{h[1], m[1], h[1], l[1], m[1], h[1], z, z};
     }
     const uint8_t* wb = buf + N.off_w0 + lane * 16;
 #pragma unroll
