@@ -1,0 +1,26 @@
+"""The bf16x3 activation split of the SPLIT kernels: every remainder
+x - (float)hi is one v_dot2c_f32_bf16, and the kernels' helper (df::uni::split2 in
+densityflows.jl_amd/csrc/df_uniform_impl.h) must give the same three bf16 planes, bit
+for bit, as the plain RNE split restated in numpy
+(tests/test_host.py::test_bf16x3_split_is_exact_and_six_products_are_f32_accurate).  The probe
+(tools/probe/dot2_split.hip, built by __graft_entry__.build()) checks 2^26 values per
+form: random f32, relu outputs, bf16 ties and near-denormals."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROBE = os.path.join(ROOT, "tools", "probe", "dot2_split")
+
+
+@pytest.mark.gpu
+def test_split_helper_planes_bitwise():
+    assert os.path.exists(PROBE), "tools/probe/dot2_split missing: run __graft_entry__.build()"
+    r = subprocess.run([PROBE], capture_output=True, text=True, timeout=60)
+    print(r.stdout)
+    lines = [l for l in r.stdout.splitlines() if l.startswith(("split2 helper", "vgpr-const"))]
+    assert len(lines) == 8, r.stdout + r.stderr
+    for l in lines:
+        assert "mismatches 0 of" in l, l
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -4,9 +4,11 @@
 // 2^24 values per pass: random magnitudes over the normal f32 range, relu outputs,
 // values near bf16 ties, tiny values near the denormal range.
 #include <hip/hip_runtime.h>
+#include "df_uniform_impl.h"  // the kernels' own split helper (df::uni::split2)
 #include <cstdio>
 #include <cstdint>
 #include <cstring>
+#include <cstdlib>
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t hash(uint32_t x) {
@@ -53,6 +55,52 @@ __global__ void k(uint32_t seed, int pass, unsigned long long* bad, uint32_t* ex
     }
 }
 
+// The product helper itself: df::uni::split2's planes (HELPER = 1) against the plain
+// RNE split (HELPER = 0), each written to memory by its own kernel and compared on the
+// host (no cross-kernel folding of the two computations).
+__device__ __forceinline__ void probe_inputs(uint32_t i, uint32_t seed, int pass, float& x0, float& x1, bool& skip) {
+    uint32_t u0 = hash(i * 2 + seed), u1 = hash(i * 2 + 1 + seed * 7919u);
+    if (pass == 1) { u0 = (u0 & 0x807fffffu) | (((u0 >> 23) % 40 + 107) << 23); u1 = (u1 & 0x807fffffu) | (((u1 >> 23) % 40 + 107) << 23); }
+    if (pass == 2) { u0 = (u0 & 0x807f0000u) | 0x8000u | (120u << 23); u1 = (u1 & 0xff7fffffu); }
+    if (pass == 3) { u0 = (u0 & 0x807fffffu) | ((1 + (u0 >> 23) % 30) << 23); u1 = (u1 & 0x807fffffu) | ((1 + (u1 >> 23) % 30) << 23); }
+    skip = (u0 & 0x7fffffffu) >= 0x7f7f8000u || (u1 & 0x7fffffffu) >= 0x7f7f8000u;
+    x0 = __uint_as_float(u0);
+    x1 = __uint_as_float(u1);
+    if (pass == 1) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+}
+
+template <int HELPER>
+__global__ void k_planes(uint32_t seed, int pass, uint32_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    float x0, x1;
+    bool skip;
+    probe_inputs(i, seed, pass, x0, x1, skip);
+    uint32_t w[3] = {0u, 0u, 0u};
+    if (!skip) {
+        if (HELPER) {
+            df::uni::bf16x2 p0, p1, p2;
+            df::uni::split2(x0, x1, p0, p1, p2);
+            w[0] = __builtin_bit_cast(uint32_t, p0);
+            w[1] = __builtin_bit_cast(uint32_t, p1);
+            w[2] = __builtin_bit_cast(uint32_t, p2);
+        } else {
+            const float x[2] = {x0, x1};
+            for (int e = 0; e < 2; ++e) {
+                const __bf16 h = (__bf16)x[e];
+                const float r = x[e] - (float)h;
+                const __bf16 m = (__bf16)r;
+                const __bf16 l = (__bf16)(r - (float)m);
+                w[0] |= (uint32_t)__builtin_bit_cast(uint16_t, h) << (16 * e);
+                w[1] |= (uint32_t)__builtin_bit_cast(uint16_t, m) << (16 * e);
+                w[2] |= (uint32_t)__builtin_bit_cast(uint16_t, l) << (16 * e);
+            }
+        }
+    }
+    out[3 * i] = w[0];
+    out[3 * i + 1] = w[1];
+    out[3 * i + 2] = w[2];
+}
+
 int main() {
     unsigned long long* bad;
     uint32_t* ex;
@@ -70,11 +118,35 @@ int main() {
         else hipLaunchKernelGGL(k<0>, dim3(1 << 16), dim3(256), 0, 0, 1234u + pass, pass, bad, ex);
         hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost);
         hipMemcpy(e, ex, 24, hipMemcpyDeviceToHost);
-        printf("%s %-28s mismatches %llu of 2^24", opq ? "vgpr-const  " : "inline-const", names[pass], nb);
+        printf("%s %-28s mismatches %llu of 2^24", opq ? "vgpr-const   " : "inline-const ", names[pass], nb);
         if (nb) printf("  e.g. x0=%08x x1=%08x r0=%08x dot=%08x l0=%08x dot=%08x", e[0], e[1], e[2], e[3], e[4], e[5]);
         printf("\n");
-        if (nb && pass < 3 && opq) rc = 1;
+        if (nb && opq) rc = 1;
     }
+    const size_t np = (size_t)1 << 24, nb = 3 * np * sizeof(uint32_t);
+    uint32_t *dh, *dp;
+    hipMalloc(&dh, nb);
+    hipMalloc(&dp, nb);
+    uint32_t* hh = (uint32_t*)malloc(nb);
+    uint32_t* hp = (uint32_t*)malloc(nb);
+    for (int pass = 0; pass < 4; ++pass) {
+        hipLaunchKernelGGL(k_planes<1>, dim3(np / 256), dim3(256), 0, 0, 1234u + pass, pass, dh);
+        hipLaunchKernelGGL(k_planes<0>, dim3(np / 256), dim3(256), 0, 0, 1234u + pass, pass, dp);
+        hipMemcpy(hh, dh, nb, hipMemcpyDeviceToHost);
+        hipMemcpy(hp, dp, nb, hipMemcpyDeviceToHost);
+        size_t bad_pairs = 0, first = 0;
+        for (size_t i = 0; i < np; ++i)
+            if (memcmp(hh + 3 * i, hp + 3 * i, 12) != 0) { if (!bad_pairs) first = i; ++bad_pairs; }
+        printf("split2 helper %-28s mismatches %zu of 2^24", names[pass], bad_pairs);
+        if (bad_pairs) printf("  e.g. pair %zu: helper %08x %08x %08x plain %08x %08x %08x", first, hh[3 * first],
+                              hh[3 * first + 1], hh[3 * first + 2], hp[3 * first], hp[3 * first + 1], hp[3 * first + 2]);
+        printf("\n");
+        if (bad_pairs) rc = 1;
+    }
+    free(hh);
+    free(hp);
+    hipFree(dh);
+    hipFree(dp);
     hipFree(bad);
     hipFree(ex);
     return rc;
