@@ -5,8 +5,8 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/${1:-sw}
 mkdir -p $O
-for kb in 80 96 112 128 160; do
-  for t in 0 2 4 6 8; do
+for kb in ${KBS:-80 96 112 128 160}; do
+  for t in ${TS:-0 2 4 6 8}; do
     if [ $t = 0 ]; then unset DF_TILES; else export DF_TILES=$t; fi
     DF_SPLIT_LDS_KB=$kb DF_DEBUG_LAUNCH=1 timeout -k 10 60 python bench.py --steps 100 --warmup 20 --no-cpu --no-exact \
         > $O/kb${kb}_t${t}.json 2> $O/kb${kb}_t${t}.err || exit 1
