@@ -32,26 +32,30 @@ __global__ void __launch_bounds__(256) mfma_16x16x4(const float* in, float* out)
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+// Inline asm, 4 chains: through the builtin the compiler shuffles the accumulators with AGPR moves
+// inside the loop.
+constexpr int kChainsBf16 = 4;
 __global__ void __launch_bounds__(256) mfma_16x16x32_bf16(const float* in, float* out) {
     bf16x8 a, b;
     for (int e = 0; e < 8; ++e) {
         a[e] = (__bf16)in[(threadIdx.x + e) & 63];
         b[e] = (__bf16)in[(threadIdx.x + 3 * e) & 63];
     }
-    f32x4 c[kChains];
-    for (int j = 0; j < kChains; ++j) c[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 c[kChainsBf16];
+    for (int j = 0; j < kChainsBf16; ++j) c[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int i = 0; i < kIters; ++i)
 #pragma unroll
-        for (int j = 0; j < kChains; ++j) c[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c[j], 0, 0, 0);
+        for (int j = 0; j < kChainsBf16; ++j)
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c[j]) : "v"(a), "v"(b));
     float s = 0.f;
-    for (int j = 0; j < kChains; ++j) s += c[j][0] + c[j][1] + c[j][2] + c[j][3];
+    for (int j = 0; j < kChainsBf16; ++j) s += c[j][0] + c[j][1] + c[j][2] + c[j][3];
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
 __global__ void __launch_bounds__(256) valu_fmac(const float* in, float* out) {
     const float a = in[threadIdx.x & 63], b = in[(threadIdx.x + 7) & 63];
     float c[kChains * 4];
-    for (int j = 0; j < kChains * 4; ++j) c[j] = in[(threadIdx.x + j) & 63];
+    for (int j = 0; j < kChains * 4; ++j) c[j] = a * (float)(j + 1);  // no loads: their waitcnts would sit in the loop
     for (int i = 0; i < kIters; ++i)
 #pragma unroll
         for (int j = 0; j < kChains * 4; ++j) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(c[j]) : "v"(a), "v"(b));
@@ -98,7 +102,7 @@ int main() {
             {"v_fmac_f32", time_ms(valu_fmac, grid, in, out), per_simd * 4},
             {"v_mfma_f32_4x4x1_16b_f32", time_ms(mfma_4x4, grid, in, out), per_simd},
             {"v_mfma_f32_16x16x4_f32 (calibration, 32)", t_16x16x4 * per_simd, per_simd},
-            {"v_mfma_f32_16x16x32_bf16", time_ms(mfma_16x16x32_bf16, grid, in, out), per_simd},
+            {"v_mfma_f32_16x16x32_bf16", time_ms(mfma_16x16x32_bf16, grid, in, out), per_simd * kChainsBf16 / kChains},
         };
         printf("CUs %d, %d wave(s) per SIMD, clock (from the 16x16x4 f32 calibration) %.0f MHz\n", cus,
                waves, cyc / 1e3);
