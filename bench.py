@@ -183,6 +183,59 @@ class _stdout_to_stderr:
         return False
 
 
+def train_split_flops(chain, kernel_id):
+    """FLOP per sample of one train! step (3F: forward, dX, dW) that the step's
+    kernels run as bf16x3 split products, from the model's Dense shapes.
+
+    Kernel 4 (FAST SPLIT, hidden <= 64 nets, fused per-net reverse kernel
+    df_train_impl.h): forward first + hidden Dense, and the hidden Dense's W1ᵀδ and
+    dW1 are split; W0ᵀδ, dW0, the output Dense GEMV, W_outᵀȳ and dW_out are f32.
+    Kernel 6 (wide SPLIT, hidden 256, layer-wise reverse path df_ltrain.hip):
+    the forward's three Denses and the hidden Dense's W1ᵀδ1 and dW1 are split,
+    the rest f32.  Every other kernel: none."""
+    from densityflows_amd.layers import RNVPCouplingLayer, NICECouplingLayer, CouplingBlock
+
+    if kernel_id not in (4, 6):
+        return 0.0
+    nets = []
+    for e in chain:
+        for layer in ([e.layer_1, e.layer_2] if isinstance(e, CouplingBlock) else [e]):
+            if isinstance(layer, RNVPCouplingLayer):
+                nets += [layer.s_net, layer.t_net]
+            elif isinstance(layer, NICECouplingLayer):
+                nets += [layer.t_net]
+    f = 0.0
+    for net in nets:
+        macs = [D.in_dim * D.out_dim for D in net]
+        hidden = sum(macs[1:-1])
+        fwd = sum(macs) if kernel_id == 6 else macs[0] + hidden
+        f += 2.0 * (fwd + 2 * hidden)
+    return f
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N ranks (one process per GPU)
+    with torch.distributed.run as a child process — before anything touches the
+    GPU — and exit with its status.  Fails loudly when fewer than N devices are
+    visible (a DF_DIST_BACKEND=gloo rehearsal may share devices)."""
+    import socket
+    import subprocess
+
+    import torch
+
+    backend = os.environ.get("DF_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()   # counts devices without initialising HIP
+    if backend == "nccl" and ndev < args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus}: only {ndev} GPU(s) visible")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, DF_BENCH_LAUNCHED="1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -198,26 +251,42 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the exact-f32 FAST kernel timing that accompanies a SPLIT-kernel bench")
+    ap.add_argument("--no-clock", action="store_true",
+                    help="do not stamp the effective shader clock of the timed launches (df_chain_clock_probe)")
+    ap.add_argument("--settle-seconds", type=float, default=0.3,
+                    help="untimed steps after the W warm-up steps until this much warm-up time has passed "
+                         "(DVFS clock ramp; 0 = exactly W)")
     ap.add_argument("--graph", action="store_true",
                     help="train mode, one rank: replay each step as one hipGraph (df_train_step_graph)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rendezvous / timing plumbing only: no library, no GPU work (CPU tests)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
 
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
+    if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    backend = os.environ.get("DF_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI
+    if args.dry_run:
+        if world > 1 and backend != "gloo":
+            raise SystemExit("--dry-run with several ranks needs DF_DIST_BACKEND=gloo")
+        return dry_run(args, world, rank)
     ndev = torch.cuda.device_count()
-    gpu = local % max(ndev, 1)          # ranks share a device only in single-GPU rehearsals
+    if backend == "nccl" and world > ndev:
+        raise SystemExit(f"WORLD_SIZE={world} ranks but only {ndev} GPU(s) visible")
+    gpu = local % max(ndev, 1)          # ranks share a device only in gloo rehearsals
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        backend = os.environ.get("DF_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI
         with _stdout_to_stderr():   # RCCL's init banner: stdout carries only the JSON line
             if backend == "nccl":
                 dist.init_process_group("nccl", device_id=dev)
@@ -225,7 +294,6 @@ def main():
                 dist.init_process_group(backend)
 
     import densityflows_amd as dfa
-    from densityflows_amd.hip import HIPChain
 
     d, n, workload = CONFIGS[args.config]
     chain = build_chain(args.config)
@@ -241,6 +309,7 @@ def main():
 
     trainer = None
     comm = None
+    probe = hc                       # the handle whose chain-pass launches carry the clock stamps
     rehearsal = dist is not None and dist.get_backend() != "nccl"   # gloo: ranks may share one GPU
     if args.mode != "forward" and not rehearsal:
         # the library's own RCCL communicator (df_comm) carries every exchange of the
@@ -274,6 +343,7 @@ def main():
     else:
         flow = dfa.Flow(chain, metadata=dfa.MetaData("", d, n, np.zeros(n, np.float32), np.ones(n, np.float32)))
         fh = flow.hip(device=gpu)
+        probe = fh
         hc.run("forward", zbuf, thbuf, xbuf, ldj, B)  # data points x = forward(z)
 
         nll = fh.lib.df_flow_nll
@@ -290,18 +360,48 @@ def main():
             if rehearsal:
                 dist.all_reduce(s64)
 
+    stream = torch.cuda.current_stream(dev)
+    steplog = os.environ.get("DF_BENCH_STEPLOG") == "1"   # diagnostic: per-step HIP-event times on stderr
+    warm_ms = []
+    if not args.no_clock:
+        probe.clock_probe(True)      # allocates the stamp slots during the warm-up
+    t_warm = time.perf_counter()
     for _ in range(args.warmup):
-        step()
+        if steplog:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            step()
+            e1.record(stream)
+            warm_ms.append((e0, e1))
+        else:
+            step()
     torch.cuda.synchronize()
+    # clock settle: the chip ramps its shader clock over the first ~50 ms of back-to-back
+    # launches (profiles/r03_clock_ramp.txt: 2.00 GHz over steps 6-25, 2.25 GHz after 50);
+    # untimed steps continue until --settle-seconds of warm-up have passed, so the K timed
+    # steps measure the steady state whatever W is (reported as clock_settle)
+    settle_steps, t_w = 0, time.perf_counter()
+    while time.perf_counter() - t_warm < args.settle_seconds and settle_steps < 100000:
+        for _ in range(8):
+            step()
+        settle_steps += 8
+        torch.cuda.synchronize()
+    settle_s = time.perf_counter() - t_w
+    if not args.no_clock:
+        probe.clock_probe(True)      # zero the stamps: they cover exactly the timed launches
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if steplog else None
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if steplog:
+            step_ev[i].record(stream)
         step()
+    if steplog:
+        step_ev[-1].record(stream)
     ev1.record(stream)
     torch.cuda.synchronize()
     if dist is not None:
@@ -309,6 +409,19 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)                 # HIP events on the launch stream
+    clock = None
+    if not args.no_clock:
+        ghz_med, ghz_mean, slots = probe.clock_read()
+        probe.clock_probe(False)
+        if slots > 0:
+            clock = {"ghz_median": round(ghz_med, 4), "ghz_sum_ratio": round(ghz_mean, 4), "workgroup_slots": slots,
+                     "kernel_mcycles_per_launch": None,
+                     "source": "in-kernel s_memtime / s_memrealtime (100 MHz) stamps by wave 0 of every workgroup of "
+                               "the timed chain-pass launches (df_chain_clock_probe)"}
+    if steplog:
+        print(json.dumps({"rank": rank, "warmup_ms": [round(a.elapsed_time(b), 4) for a, b in warm_ms],
+                          "step_ms": [round(step_ev[i].elapsed_time(step_ev[i + 1]), 4) for i in range(args.steps)]}),
+              file=sys.stderr, flush=True)
     elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
     if dist is not None:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
@@ -316,20 +429,23 @@ def main():
     total = B * world * args.steps
     value = total / elapsed / 1e6
     kernel_s = gpu_ms / 1e3 / args.steps            # mean launch time (one launch per step)
+    if clock is not None and args.mode != "train":
+        # clock-normalised time: shader cycles per launch (comparable across boxes and DVFS states)
+        clock["kernel_mcycles_per_launch"] = round(kernel_s * clock["ghz_median"] * 1e3, 4)
     flop = info.flops_per_sample * B
     achieved_tflops = flop / kernel_s / 1e12
     hbm_algo = (8.0 * d + 4.0 * n + 4.0) * B          # read z (+θ), write x, ldj
+
+    # roofline peak of the arithmetic the kernels run: the SPLIT kernels compute their
+    # GEMMs on bf16 MFMA (six products per f32 product), the rest on f32 MFMA / VALU
+    kernel_id = int(getattr(info, "kernel", 3))
+    f_all = float(info.flops_per_sample)
+    f_split = float(getattr(info, "split_flops_per_sample", 0.0))
     if args.mode == "train":
         # algorithmic training work: forward + 2× backward (dX and dW) = 3F per sample
-        flop = 3.0 * info.flops_per_sample * B
-        achieved_tflops = flop / kernel_s / 1e12
-
-    # roofline peak of the arithmetic the kernel runs: the SPLIT kernel computes its
-    # first and hidden Dense GEMMs on bf16 MFMA (six products per f32 product), the
-    # output Dense as an f32 VALU GEMV; every other kernel is exact f32 MFMA
-    kernel_id = int(getattr(info, "kernel", 3))
-    f_split = float(getattr(info, "split_flops_per_sample", 0.0)) if args.mode != "train" else 0.0
-    f_all = float(info.flops_per_sample)
+        f_all = 3.0 * f_all
+        f_split = train_split_flops(chain, kernel_id)
+        achieved_tflops = f_all * B / kernel_s / 1e12
     peak = PEAK_F32_TFLOPS
     if f_split > 0.0:
         peak = f_all / (f_split / PEAK_SPLIT_TFLOPS + (f_all - f_split) / PEAK_F32_TFLOPS)
@@ -397,9 +513,14 @@ def main():
                          if pmc.get("source") else None,
                          "kernel_ms": round(kernel_s * 1e3, 4),
                          "kernel_ms_scope": "whole step (all launches)" if args.mode == "train" else "one launch",
-                         "algorithmic_flop_per_sample": info.flops_per_sample,
+                         "algorithmic_flop_per_sample": f_all,
                          "hbm_algorithmic_GBps": round(hbm_algo / kernel_s / 1e9, 2)},
+            "clock": clock,
+            "clock_settle": {"untimed_steps_after_warmup": settle_steps, "seconds": round(settle_s, 3),
+                             "target_seconds_of_warmup": args.settle_seconds},
         }
+        if args.mode == "train" and clock is not None:
+            clock["scope"] = "the inverse chain pass of each step only"
         if args.config != "cfg2":
             out["metric"] = out["metric"].replace("d=5 8-layer RealNVP", CONFIGS[args.config][2].split(":")[0])
         if exact is not None:
@@ -415,6 +536,36 @@ def main():
         assert s64[1].item() == B * world and np.isfinite(loss), "df_flow_nll returned an inconsistent {Σ, N}"
     if comm is not None:
         comm.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def dry_run(args, world, rank):
+    """The bench's launch, rendezvous and max-over-ranks timing without the
+    library or a GPU: tests of `--gpus N` self-launching run it on CPU (gloo)."""
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+    for _ in range(args.warmup):
+        pass
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    if dist is not None:
+        dist.barrier()
+    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if dist is not None:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Msamples/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                          "ms_per_step": float(elapsed.item()) * 1e3 / max(args.steps, 1)}), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

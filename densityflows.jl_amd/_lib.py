@@ -145,6 +145,8 @@ SIGNATURES = {
     "df_flow_nll": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _VP]),
     "df_train_allreduce_gradient": (C.c_int, [_VP, _VP, _VP]),
     "df_train_step_dist": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _I64, _VP, _VP]),
+    "df_chain_clock_probe": (C.c_int, [_VP, C.c_int]),
+    "df_chain_clock_read": (C.c_int, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(_I64)]),
     "df_device_alloc": (C.c_int, [C.POINTER(_VP), C.c_size_t]),
     "df_device_free": (C.c_int, [_VP]),
     "df_memcpy_h2d": (C.c_int, [_VP, _VP, C.c_size_t, _VP]),

@@ -4,6 +4,7 @@
 // of it, and launches the fused kernels (df_kernels_ht*.hip).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -130,7 +131,7 @@ int df_chain_destroy(df_chain* c) {
                     c->d_params, c->d_bounds, c->d_partial, c->d_sched,   c->d_ulayers, c->d_wlayers,
                     c->d_wstages, c->d_wblob, c->d_wbias,  c->d_wsched, c->d_sblob, c->d_sstages,
                     c->d_ssched,  c->d_sulayers, c->d_wslayers, c->d_wsstages, c->d_wsblob, c->d_wssched,
-                    c->d_wstables};
+                    c->d_wstables, c->d_clk};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;
@@ -433,7 +434,18 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
         c->partial_gen++;
     }
 
+    if (c->clk_on && grid > c->clk_cap) {  // stamp slots for this grid (zeroed: a new series)
+        if (c->d_clk) (void)hipFree(c->d_clk);
+        c->d_clk = nullptr;
+        c->clk_cap = 0;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->d_clk), sizeof(uint64_t) * 2 * grid);
+        if (e == hipSuccess) e = hipMemsetAsync(c->d_clk, 0, sizeof(uint64_t) * 2 * grid, (hipStream_t)stream);
+        if (e != hipSuccess) return set_err(DF_ERR_NOMEM, "hipMalloc failed (clock stamps)");
+        c->clk_cap = grid;
+    }
+
     df::ChainArgs a{};
+    a.clk = c->clk_on ? c->d_clk : nullptr;
     a.zin = zin;
     a.theta = theta;
     a.xout = xout;
@@ -563,6 +575,48 @@ int df_flow_logpdf_sum(df_chain* c, const float* x, const float* theta_raw, doub
                        void* stream) {
     if (!sum_out) return set_err(DF_ERR_INVALID, "null sum output");
     return run(c, df::MODE_LOGPDF, true, x, theta_raw, nullptr, nullptr, nullptr, sum_out, batch, stream);
+}
+
+int df_chain_clock_probe(df_chain* c, int on) {
+    if (!c) return set_err(DF_ERR_INVALID, "null chain");
+    DeviceGuard gd(c->device);
+    if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
+    if (on && c->d_clk) {
+        hipError_t e = hipDeviceSynchronize();
+        if (e == hipSuccess) e = hipMemset(c->d_clk, 0, sizeof(uint64_t) * 2 * c->clk_cap);
+        if (e != hipSuccess) return hip_err(e, "hipMemset(clock stamps)");
+    }
+    c->clk_on = on != 0;
+    return DF_OK;
+}
+
+int df_chain_clock_read(df_chain* c, double* ghz_median, double* ghz_mean, int64_t* n_slots) {
+    if (!c || !ghz_median || !ghz_mean || !n_slots) return set_err(DF_ERR_INVALID, "null pointer");
+    *ghz_median = *ghz_mean = 0.0;
+    *n_slots = 0;
+    if (!c->d_clk || c->clk_cap == 0) return DF_OK;
+    DeviceGuard gd(c->device);
+    if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
+    std::vector<uint64_t> h((size_t)2 * c->clk_cap);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(h.data(), c->d_clk, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_err(e, "hipMemcpy(clock stamps)");
+    std::vector<double> ghz;
+    double st = 0.0, sr = 0.0;
+    for (int64_t b = 0; b < c->clk_cap; ++b) {
+        const uint64_t dt = h[2 * b], dr = h[2 * b + 1];
+        if (dr == 0) continue;
+        ghz.push_back(0.1 * (double)dt / (double)dr);  // s_memrealtime ticks at 100 MHz
+        st += (double)dt;
+        sr += (double)dr;
+    }
+    if (ghz.empty()) return DF_OK;
+    std::sort(ghz.begin(), ghz.end());
+    const size_t m = ghz.size();
+    *ghz_median = (m & 1) ? ghz[m / 2] : 0.5 * (ghz[m / 2 - 1] + ghz[m / 2]);
+    *ghz_mean = 0.1 * st / sr;
+    *n_slots = (int64_t)m;
+    return DF_OK;
 }
 
 int df_device_alloc(void** ptr, size_t bytes) {

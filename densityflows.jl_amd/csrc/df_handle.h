@@ -60,6 +60,10 @@ struct df_chain {
     void* d_wstables = nullptr;
     int wstab_bytes = 0;
     size_t wslds = 0;
+    // effective-clock stamps (df_chain_clock_probe): 2 × uint64 per workgroup slot
+    uint64_t* d_clk = nullptr;
+    int64_t clk_cap = 0;  // workgroup slots
+    bool clk_on = false;
 };
 
 // SPLIT launches unless DF_F32_EXACT=1 (read per launch: an A/B knob for tests and benches)

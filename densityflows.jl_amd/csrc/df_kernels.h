@@ -49,6 +49,31 @@ struct ChainArgs {
     int hsave_w, hsave_h;
     const WLayer* wlayers;   // wide-net kernel only (stages / blob / schedules then refer to the wide blob)
     const float* wbias;
+    uint64_t* clk;           // effective-clock stamps (df_chain_clock_probe), nullptr = off
+};
+
+// Effective shader clock of a launch (df_chain_clock_probe): wave 0 of every
+// workgroup adds Δs_memtime (shader cycles) and Δs_memrealtime (100 MHz ticks)
+// over its lifetime to clk[2·blockIdx.x + {0, 1}].  Launches on one stream do
+// not overlap, so the read-modify-write needs no atomics; the values go to a
+// buffer nothing else reads.  Off (clk == nullptr): one scalar branch per end.
+struct ClockStamp {
+    uint64_t t0 = 0, r0 = 0;
+    __device__ __forceinline__ void begin(const ChainArgs& a) {
+        if (a.clk) {
+            t0 = __builtin_amdgcn_s_memtime();
+            r0 = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    __device__ __forceinline__ void end(const ChainArgs& a) {
+        if (a.clk && threadIdx.x == 0) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+            uint64_t* p = a.clk + 2 * (uint64_t)blockIdx.x;
+            p[0] += t1 - t0;
+            p[1] += r1 - r0;
+        }
+    }
 };
 
 // Per-variant entry points (explicitly instantiated in df_kernels_ht*.hip).

@@ -574,6 +574,8 @@ uniform_kernel(ChainArgs a) {
     int32_t* tab = reinterpret_cast<int32_t*>(smem + stage_area);
     float* state = reinterpret_cast<float*>(smem + stage_area + a.tab_bytes);
 
+    ClockStamp clk;
+    clk.begin(a);
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, j = lane & 15;
@@ -738,7 +740,10 @@ uniform_kernel(ChainArgs a) {
                 a.partial[blockIdx.x] = s;
             }
         }
-        if (!a.xout) return;
+        if (!a.xout) {
+            clk.end(a);
+            return;
+        }
     }
     __syncthreads();
     for (int i = tid; i < S * d; i += kBlockThreads) {
@@ -748,6 +753,7 @@ uniform_kernel(ChainArgs a) {
     if (WANT_LDJ && MODE != MODE_LOGPDF && a.ldj_out) {
         for (int i = tid; i < nvalid; i += kBlockThreads) a.ldj_out[s0 + i] = state[i * stride + cA];
     }
+    clk.end(a);
 }
 
 template <int HT, bool RELU, bool FAST = false, bool SPLIT = false>

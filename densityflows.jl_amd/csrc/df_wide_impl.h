@@ -580,6 +580,8 @@ __global__ void __launch_bounds__(SPLIT ? wide::kSplitWaves * 64 : wide::kThread
     constexpr int TT = SPLIT ? kSplitT : T;               // 16-sample tiles per wave
     constexpr int NT = NW * 64;
 
+    ClockStamp clk;
+    clk.begin(a);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NB = SPLIT ? kWideSplitBufs : kWideBufs;  // ring slots
     const int stage_area = NB * SBYTES;
@@ -740,7 +742,10 @@ __global__ void __launch_bounds__(SPLIT ? wide::kSplitWaves * 64 : wide::kThread
                 a.partial[blockIdx.x] = s;
             }
         }
-        if (!a.xout) return;
+        if (!a.xout) {
+            clk.end(a);
+            return;
+        }
     }
     __syncthreads();
     for (int i = tid; i < S * d; i += NT) {
@@ -750,6 +755,7 @@ __global__ void __launch_bounds__(SPLIT ? wide::kSplitWaves * 64 : wide::kThread
     if (WANT_LDJ && MODE != MODE_LOGPDF && a.ldj_out) {
         for (int i = tid; i < nvalid; i += NT) a.ldj_out[s0 + i] = state[i * stride + cA];
     }
+    clk.end(a);
 }
 
 }  // namespace df

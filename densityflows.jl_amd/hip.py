@@ -232,6 +232,18 @@ class HIPChain:
             self.handle, tmin.ctypes.data_as(C.POINTER(C.c_float)), tmax.ctypes.data_as(C.POINTER(C.c_float))))
         self.bounds = (tmin.copy(), tmax.copy())
 
+    # -- diagnostics ---------------------------------------------------------
+    def clock_probe(self, on: bool = True) -> None:
+        """df_chain_clock_probe: stamp the effective shader clock of later passes."""
+        _lib.check(self.lib.df_chain_clock_probe(self.handle, 1 if on else 0), "df_chain_clock_probe")
+
+    def clock_read(self):
+        """df_chain_clock_read → (median GHz over workgroup slots, Σcycles/Σtime GHz, slots)."""
+        med, mean, slots = C.c_double(), C.c_double(), C.c_int64()
+        _lib.check(self.lib.df_chain_clock_read(self.handle, C.byref(med), C.byref(mean), C.byref(slots)),
+                   "df_chain_clock_read")
+        return med.value, mean.value, slots.value
+
     # -- raw entry points on flat device buffers ---------------------------
     def run(self, op: str, zbuf, thbuf, outbuf, ldjbuf, batch: int, flow: bool = False):
         fn = {

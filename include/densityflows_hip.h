@@ -317,6 +317,19 @@ int df_train_allreduce_gradient(df_train* t, df_comm* comm, void* stream);
 int df_train_step_dist(df_train* t, df_comm* comm, const float* x, const float* theta_raw, int64_t batch,
                        int64_t n_total, double* logpdf_sum, void* stream);
 
+/* ---- diagnostics (no reference counterpart) ---------------------------------
+ * Effective shader clock of the fused chain-pass kernels, the evidence behind a
+ * clock-normalised benchmark time (the chip lowers its clock under load, and
+ * devices differ).  on = 1 zeroes the stamp buffer and makes every later chain
+ * pass of this handle that runs the specialised (kernels 1-4) or wide (5, 6)
+ * kernel accumulate, per workgroup, Δs_memtime (shader cycles) and
+ * Δs_memrealtime (100 MHz ticks) over its wave 0's lifetime; on = 0 stops.
+ * df_chain_clock_read synchronises the device and returns the median over
+ * workgroup slots and the ratio of sums (GHz), and the number of slots
+ * stamped (0: nothing stamped yet). */
+int df_chain_clock_probe(df_chain* chain, int on);
+int df_chain_clock_read(df_chain* chain, double* ghz_median, double* ghz_mean, int64_t* n_slots);
+
 /* ---- device memory helpers (for hosts without a GPU array package) ------ */
 int df_device_alloc(void** ptr, size_t bytes);
 int df_device_free(void* ptr);
