@@ -452,8 +452,17 @@ def main():
 
     exact = None
     if kernel_id in (4, 6) and args.mode == "forward" and not args.no_exact:
-        # the same launches on the exact-f32 FAST kernel (DF_F32_EXACT is read per launch)
+        # the same launches on the exact-f32 kernel: a second handle planned under
+        # DF_F32_EXACT=1 (a chain's arithmetic is fixed when it is created)
+        from densityflows_amd.hip import HIPChain
+
         os.environ["DF_F32_EXACT"] = "1"
+        hx = HIPChain(chain.layers, device=gpu, n_hint=n)
+        del os.environ["DF_F32_EXACT"]
+
+        def step():
+            hx.run("forward", zbuf, thbuf, xbuf, ldj, B)
+
         for _ in range(min(args.warmup, 20)):
             step()
         torch.cuda.synchronize()
@@ -466,7 +475,6 @@ def main():
             step()
         e1.record(stream)
         torch.cuda.synchronize()
-        del os.environ["DF_F32_EXACT"]
         ms = e0.elapsed_time(e1) / k_exact
         exact = {"kernel": KERNELS[kernel_id - 1], "ms_per_step": round(ms, 4), "value": round(B * world / ms / 1e3, 3),
                  "frac_of_f32_peak": round(f_all * B / (ms / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4), "steps": k_exact}

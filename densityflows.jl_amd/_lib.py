@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdensityflows_hip.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # df_status
 DF_OK = 0
@@ -145,6 +145,8 @@ SIGNATURES = {
     "df_flow_nll": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _VP]),
     "df_train_allreduce_gradient": (C.c_int, [_VP, _VP, _VP]),
     "df_train_step_dist": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _I64, _VP, _VP]),
+    "df_flow_sample": (C.c_int, [_VP, _VP, _VP, C.c_int, _I64, C.c_uint64, C.c_uint64, _VP]),
+    "df_random_normal": (C.c_int, [_VP, _I64, C.c_uint64, C.c_uint64, _VP]),
     "df_chain_clock_probe": (C.c_int, [_VP, C.c_int]),
     "df_chain_clock_read": (C.c_int, [_VP, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(_I64)]),
     "df_device_alloc": (C.c_int, [C.POINTER(_VP), C.c_size_t]),

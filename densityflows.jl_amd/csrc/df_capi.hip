@@ -47,17 +47,11 @@ static int uniform_variant(const df::Plan& P, bool split = false) {
     return P.uniform ? (P.fast ? (split ? 4 : 3) : P.relu_only ? 2 : 1) : 0;
 }
 
-bool use_split(const df_chain* c) {
-    if (!c->plan.split) return false;
-    const char* e = std::getenv("DF_F32_EXACT");
-    return !(e && e[0] == '1');
-}
+// The SPLIT blobs exist only when the chain was planned without DF_F32_EXACT=1
+// (build_split / build_wide_split read it once, at df_chain_create).
+bool use_split(const df_chain* c) { return c->plan.split && !c->exact; }
 
-bool use_wsplit(const df_chain* c) {
-    if (!c->plan.wsplit) return false;
-    const char* e = std::getenv("DF_F32_EXACT");
-    return !(e && e[0] == '1');
-}
+bool use_wsplit(const df_chain* c) { return c->plan.wsplit && !c->exact; }
 
 static size_t lds_for_tiles(const df_chain* c, int t, bool split = false) {
     const df::Plan& P = c->plan;
@@ -131,7 +125,7 @@ int df_chain_destroy(df_chain* c) {
                     c->d_params, c->d_bounds, c->d_partial, c->d_sched,   c->d_ulayers, c->d_wlayers,
                     c->d_wstages, c->d_wblob, c->d_wbias,  c->d_wsched, c->d_sblob, c->d_sstages,
                     c->d_ssched,  c->d_sulayers, c->d_wslayers, c->d_wsstages, c->d_wsblob, c->d_wssched,
-                    c->d_wstables, c->d_clk};
+                    c->d_wstables, c->d_clk, c->d_theta_ws};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;
@@ -148,7 +142,9 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
     df_chain* c = new (std::nothrow) df_chain();
     if (!c) return set_err(DF_ERR_NOMEM, "host allocation failed");
     std::string err;
-    int rc = df::build_plan(desc, &c->plan, &err);
+    const char* ex = std::getenv("DF_F32_EXACT");   // the chain's arithmetic, read once
+    c->exact = ex && ex[0] == '1';
+    int rc = df::build_plan(desc, &c->plan, &err, c->exact ? 1 : 0);
     if (rc != DF_OK) {
         delete c;
         return set_err(rc, err);
@@ -313,7 +309,7 @@ int df_chain_set_weights(df_chain* c, const df_chain_desc* desc) {
                                        "(use df_train_set_params)");
     df::Plan P;
     std::string err;
-    int rc = df::build_plan(desc, &P, &err);
+    int rc = df::build_plan(desc, &P, &err, c->exact ? 1 : 0);   // the chain's arithmetic, not today's env
     if (rc != DF_OK) return set_err(rc, err);
     const df::Plan& Q = c->plan;
     // structure: everything but the parameter values (and the ldj constants of the

@@ -15,6 +15,7 @@
 struct df_chain {
     df::Plan plan;
     int device = 0;
+    bool exact = false;         // DF_F32_EXACT=1 at df_chain_create: exact-f32 kernels only (read once)
     void* d_layers = nullptr;
     void* d_denses = nullptr;
     void* d_chunks = nullptr;
@@ -64,9 +65,12 @@ struct df_chain {
     uint64_t* d_clk = nullptr;
     int64_t clk_cap = 0;  // workgroup slots
     bool clk_on = false;
+    // θ broadcast workspace of df_flow_sample (NTuple θ)
+    float* d_theta_ws = nullptr;
+    int64_t theta_ws_cap = 0;
 };
 
-// SPLIT launches unless DF_F32_EXACT=1 (read per launch: an A/B knob for tests and benches)
+// SPLIT launches unless the chain was created under DF_F32_EXACT=1 (df_chain::exact)
 bool use_split(const df_chain* c);
 bool use_wsplit(const df_chain* c);
 

@@ -123,8 +123,6 @@ void check_net(const df_dense_desc* net, int nd, int in_dim, int out_dim, const 
 void build_split(const df_chain_desc* desc, Plan& P, const std::vector<char>& fold) {
     P.split = 0;
     if (!P.fast || (P.ht != 2 && P.ht != 4)) return;
-    if (const char* e = std::getenv("DF_F32_EXACT"))
-        if (e[0] == '1') return;
     const int ht = P.ht, H = 16 * ht;
     auto net_bytes = [&](int n_out) {
         return kSplitFirstBytes(ht) + kSplitHiddenBytes(ht) + 4 * H + round_up((n_out * H + 4) * 4, 16);
@@ -442,8 +440,6 @@ void build_wide(const df_chain_desc* desc, Plan& P) {
 void build_wide_split(const df_chain_desc* desc, Plan& P) {
     P.wsplit = 0;
     if (!P.wide) return;
-    if (const char* e = std::getenv("DF_F32_EXACT"))
-        if (e[0] == '1') return;
     P.wstables = P.tables;
     P.wslayers = P.wlayers;
     const int zero_slot = P.n + P.d;
@@ -537,10 +533,11 @@ size_t plan_lds_bytes(const Plan& p) {
     return (size_t)nbuf * p.stage_max + tab + (size_t)p.samples_per_block * p.stride * 4;
 }
 
-int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
+int build_plan(const df_chain_desc* desc, Plan* out, std::string* err, int exact) {
     try {
         if (!desc || !out) fail(DF_ERR_INVALID, "null descriptor");
-        if (desc->abi_version != DF_ABI_VERSION) fail(DF_ERR_INVALID, "ABI version mismatch");
+        // the descriptor structs are unchanged since ABI 2 (ABI 3 added entry points only)
+        if (desc->abi_version < 2 || desc->abi_version > DF_ABI_VERSION) fail(DF_ERR_INVALID, "ABI version mismatch");
         const int d = desc->d, n = desc->n;
         if (d < 1 || n < 0) fail(DF_ERR_INVALID, "d must be >= 1 and n >= 0");
         if (n + d > kMaxState) fail(DF_ERR_UNSUPPORTED, "n + d > 64 is outside the fused kernel's limits");
@@ -1081,9 +1078,13 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err) {
             P.stage_max = 0;
         }
         P.blob.resize(round_up((int)P.blob.size(), 16) + 16, 0);
-        build_split(desc, P, fold);
+        if (exact < 0) {
+            const char* e = std::getenv("DF_F32_EXACT");
+            exact = (e && e[0] == '1') ? 1 : 0;
+        }
+        if (!exact) build_split(desc, P, fold);
         build_wide(desc, P);
-        build_wide_split(desc, P);
+        if (!exact) build_wide_split(desc, P);
         *out = std::move(P);
         return DF_OK;
     } catch (const Fail& f) {

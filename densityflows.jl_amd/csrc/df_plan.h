@@ -254,7 +254,8 @@ struct Plan {
 
 // Returns DF_OK or a df_status; *err receives a message mirroring the
 // reference's exception text where one exists.
-int build_plan(const df_chain_desc* desc, Plan* out, std::string* err);
+// exact: plan the exact-f32 kernels only (no SPLIT blobs); -1 = from DF_F32_EXACT
+int build_plan(const df_chain_desc* desc, Plan* out, std::string* err, int exact = -1);
 
 // Workgroup LDS bytes for a plan (stage buffers + tables + state tile).
 size_t plan_lds_bytes(const Plan& p);

@@ -212,8 +212,7 @@ LOp pack_lop(df_train* t, const Plan& P, const LDense& D, bool transposed) {
                     t->lsrc.push_back((int32_t)src);
                 }
     // SPLIT planes of a hidden-256 Wᵀ (the ldense_kernel SPLIT instances)
-    const char* ex = std::getenv("DF_F32_EXACT");
-    if (transposed && op.mt == 16 && op.nkq % 2 == 0 && !(ex && ex[0] == '1')) {
+    if (transposed && op.mt == 16 && op.nkq % 2 == 0 && !t->c->exact) {
         op.sfrag = (int64_t)t->lsblob.size();
         t->lsblob.resize(t->lsblob.size() + (size_t)(op.nkq / 2) * op.mt * 3072, 0);
         for (int c = 0; c < op.nkq / 2; ++c)
@@ -384,8 +383,7 @@ int build_nets(df_train* t) {
             g.p_count = end - g.p_begin;
             pack_transposed(t, P, g, D0, D1, ht);
             // SPLIT: the net's region of the chain's SPLIT blob and its W1ᵀ planes
-            const char* ex = std::getenv("DF_F32_EXACT");
-            if (P.split && D1 && t->amode == trn::AM_RELU && (ht == 2 || ht == 4) && !(ex && ex[0] == '1')) {
+            if (use_split(t->c) && D1 && t->amode == trn::AM_RELU && (ht == 2 || ht == 4)) {
                 const ULayer& SU = P.sulayers[li];
                 const UNet& s0 = (phase == TR_PHASE_S) ? SU.s : SU.t;
                 const int slo = s0.off_w0;
@@ -545,8 +543,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
     const uint8_t* lb = static_cast<const uint8_t*>(t->d_lblob);
     const float* lbf = static_cast<const float*>(t->d_lblob);
     const uint8_t* lsb = static_cast<const uint8_t*>(t->d_lsblob);
-    const char* ex = std::getenv("DF_F32_EXACT");
-    const bool lsplit = !(ex && ex[0] == '1');
+    const bool lsplit = !c->exact;   // the chain's arithmetic, fixed at df_chain_create
     auto sfrag_of = [&](const LOp& op, int in_kind, int epi) -> const uint8_t* {
         return (lsplit && op.sfrag >= 0 && ldense_split_supported(op.mt, in_kind, epi)) ? lsb + op.sfrag : nullptr;
     };

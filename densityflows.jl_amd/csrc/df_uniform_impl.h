@@ -424,6 +424,59 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& p0, bf16x8& 
     }
 }
 
+// Remainders on the matrix pipe (DF_SPLIT_MREM): for one accumulator tile c (lane
+// (g, j): rows 4g + r of sample j) and its RNE bf16 plane h (the same four values),
+// v_mfma_f32_16x16x16_bf16 with A = −I and C = c gives c − h: the only non-zero
+// product is −h, exact, and C + one product rounds once — to the exact difference
+// (representable: h is c rounded to 8 significant bits).  Bitwise the dot2 remainder,
+// one matrix instruction per 16 values instead of 16 v_dot2c_f32_bf16 (which cost
+// ≈ 8–10 issue cycles each beside the MFMAs).  −I on the A operand: lane (g, i) holds
+// A[i][4g + e], −1 iff 4g + e == i.  (A non-finite value of one row turns 0·inf into
+// NaN for its whole sample — whose outputs are non-finite anyway.)
+#ifndef DF_SPLIT_MREM
+#define DF_SPLIT_MREM 1
+#endif
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ short4v neg_eye() {
+    const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    short4v p;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p[e] = (4 * g + e == i) ? (short)0xbf80 : (short)0;
+    return p;
+}
+
+__device__ __forceinline__ f32x4 mrem(short4v eye, bf16x4v h, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(eye, __builtin_bit_cast(short4v, h), c, 0, 0, 0);
+}
+
+// planes of two accumulator tiles (8 values: a then b), remainders on the matrix pipe
+__device__ __forceinline__ void split8_mrem(short4v eye, const f32x4& a, const f32x4& b, bf16x8& p0, bf16x8& p1,
+                                            bf16x8& p2) {
+    bf16x4v h0, h1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        h0[e] = (__bf16)a[e];
+        h1[e] = (__bf16)b[e];
+    }
+    p0 = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+    const f32x4 ra = mrem(eye, h0, a), rb = mrem(eye, h1, b);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        h0[e] = (__bf16)ra[e];
+        h1[e] = (__bf16)rb[e];
+    }
+    p1 = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+    const f32x4 sa = mrem(eye, h0, ra), sb = mrem(eye, h1, rb);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        h0[e] = (__bf16)sa[e];
+        h1[e] = (__bf16)sb[e];
+    }
+    p2 = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 // First Dense of a FAST net (one k-step, bias folded in slot g = 3): lane group g
 // carries feature g's planes in the product slots (x0, x1, x0, x2, x1, x0, 0, 0)
 // against the planner's (w0, w0, w1, w0, w1, w2, 0, 0): one MFMA per m-tile.
@@ -460,6 +513,7 @@ __device__ __forceinline__ void dense_hidden_split(const uint8_t* wb, const f32x
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const uint8_t* bb = wb + (HT / 2) * HT * 3072;
     wb += lane * 16;
+    const short4v eye = DF_SPLIT_MREM ? neg_eye() : short4v{0, 0, 0, 0};
 #pragma unroll
     for (int m = 0; m < HT; ++m) {
         const f32x4 b = BIAS ? lds4(bb + ((16 * m + 4 * g) << 2)) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -473,7 +527,14 @@ __device__ __forceinline__ void dense_hidden_split(const uint8_t* wb, const f32x
         for (int t = 0; t < TT; ++t) {
             const float v[8] = {in[t][2 * c][0],     in[t][2 * c][1],     in[t][2 * c][2],     in[t][2 * c][3],
                                 in[t][2 * c + 1][0], in[t][2 * c + 1][1], in[t][2 * c + 1][2], in[t][2 * c + 1][3]};
-            split8(v, x[t][0], x[t][1], x[t][2]);
+#ifdef DF_DIAG_NOSPLIT  // diagnostic build: hi plane only, repeated (results are wrong)
+            for (int e = 0; e < 8; ++e) x[t][0][e] = (__bf16)v[e];
+            x[t][1] = x[t][0];
+            x[t][2] = x[t][0];
+#else
+            if constexpr (DF_SPLIT_MREM) split8_mrem(eye, in[t][2 * c], in[t][2 * c + 1], x[t][0], x[t][1], x[t][2]);
+            else split8(v, x[t][0], x[t][1], x[t][2]);
+#endif
         }
 #pragma unroll
         for (int m = 0; m < HT; ++m) {

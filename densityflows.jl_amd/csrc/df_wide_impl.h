@@ -404,13 +404,24 @@ __device__ __forceinline__ void split_chunk(const uint8_t* buf, const bf16x8 (&x
 }
 
 // Planes of accumulator tiles 2c, 2c+1 (inputs 32c + 16(e>>2) + 4g + (e&3)).
+// DF_WIDE_MREM: the remainders on the matrix pipe (uni::split8_mrem, bitwise split8).  Off:
+// this kernel is matrix-pipe bound at one wave per SIMD, and the extra 16x16x16 MFMAs cost
+// more than the v_dot2c they replace (config-4 forward 35.7 vs 37.3 Msamples/s).
+#ifndef DF_WIDE_MREM
+#define DF_WIDE_MREM 0
+#endif
 template <int TT>
 __device__ __forceinline__ void split_tiles(const f32x4 (&h)[TT][16], int c, bf16x8 (&x)[TT][3]) {
+    const uni::short4v eye = uni::neg_eye();
 #pragma unroll
     for (int t = 0; t < TT; ++t) {
-        const float v[8] = {h[t][2 * c][0],     h[t][2 * c][1],     h[t][2 * c][2],     h[t][2 * c][3],
-                            h[t][2 * c + 1][0], h[t][2 * c + 1][1], h[t][2 * c + 1][2], h[t][2 * c + 1][3]};
-        split8(v, x[t][0], x[t][1], x[t][2]);
+        if constexpr (DF_WIDE_MREM) {
+            uni::split8_mrem(eye, h[t][2 * c], h[t][2 * c + 1], x[t][0], x[t][1], x[t][2]);
+        } else {
+            const float v[8] = {h[t][2 * c][0],     h[t][2 * c][1],     h[t][2 * c][2],     h[t][2 * c][3],
+                                h[t][2 * c + 1][0], h[t][2 * c + 1][1], h[t][2 * c + 1][2], h[t][2 * c + 1][3]};
+            split8(v, x[t][0], x[t][1], x[t][2]);
+        }
     }
 }
 

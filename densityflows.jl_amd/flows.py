@@ -11,7 +11,7 @@ import numpy as np
 from . import _lib
 from .chains import FlowChain, _n_of
 from .data import DataArrays, MetaData, maximum_theta, minimum_theta
-from .hip import julia_empty
+from .hip import as_julia_device, julia_empty
 
 __all__ = ["Flow", "MvNormal", "predict", "sample", "logpdf", "pdf", "training_loss", "validation_loss",
            "nll_partial_sum"]
@@ -107,33 +107,41 @@ def predict(flow: Flow, z, theta=None):
     return flow.forward(z, theta)[0]
 
 
-def sample(flow: Flow, dims: Union[int, Tuple[int, ...]], theta=None, generator=None):
-    """``sample(flow, dims [, θ])`` — src/Flows.jl:157-192.
-
-    Draws r ~ MvNormal(0, I) on the device (torch Philox stream; Julia's
-    Xoshiro stream cannot be matched) with shape (d, dims...) in Julia memory
-    order, then applies the fused ``forward!``.  θ may be an array
-    (n, dims...) or an NTuple broadcast to every point."""
+def sample(flow: Flow, dims: Union[int, Tuple[int, ...]], theta=None, rng=None, seed: Optional[int] = None,
+           offset: int = 0):
+    """``sample([rng, ] flow, dims [, θ])`` — src/Flows.jl:157-192, one library call
+    (``df_flow_sample``): r ~ MvNormal(0, I) drawn on the device from a Philox4x32-10
+    stream keyed by ``seed`` (default: 64 bits drawn from ``rng``, a
+    ``numpy.random.Generator``, as Julia draws from its ``rng``; Julia's Xoshiro
+    stream itself is not reproduced), shape (d, dims...) in Julia memory order,
+    then the fused ``forward!`` with θ normalised in the kernel.  θ: an array
+    (n, dims...) or an NTuple broadcast to every point (Flows.jl:178-188)."""
     import torch
 
     if isinstance(dims, int):
         dims = (dims,)
     dims = tuple(int(v) for v in dims)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    if seed is None:
+        rng = rng if rng is not None else np.random.default_rng()
+        seed = int(rng.integers(0, 2**63 - 1, dtype=np.int64)) * 2 + int(rng.integers(0, 2))
+    h = flow.hip()
+    dev = h.device
     buf, r = julia_empty(flow.d, dims, dev)
-    buf.normal_(0.0, 1.0, generator=generator)
+    batch = int(np.prod(dims)) if dims else 1
+    thb, bcast = None, False
     if flow.n > 0:
         if theta is None:
             raise AssertionError("dimensions θ must match (n, dims...) with n number of trained parameters")
-        if not isinstance(theta, tuple):
-            th = theta
-            if tuple(th.shape) != (flow.n,) + dims:
+        if isinstance(theta, tuple):
+            if len(theta) != flow.n:
                 raise AssertionError("dimensions θ must match (n, dims...) with n number of trained parameters")
+            thb = torch.tensor([float(np.float32(v)) for v in theta], dtype=torch.float32, device=dev)
+            bcast = True
         else:
-            th = _broadcast_theta(theta, dims, r)
-    else:
-        th = None
-    flow.forward_(r, th)
+            if tuple(theta.shape) != (flow.n,) + dims:
+                raise AssertionError("dimensions θ must match (n, dims...) with n number of trained parameters")
+            thb, _, _ = as_julia_device(theta, flow.n, dev, "θ")
+    h.run_sample(buf, thb, bcast, batch, seed, offset)
     return r
 
 

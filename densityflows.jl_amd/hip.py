@@ -266,6 +266,17 @@ class HIPChain:
                                                C.c_void_p(sumbuf.data_ptr()), C.c_int64(batch),
                                                _stream(self.device)), "logpdf_sum")
 
+    def run_sample(self, xbuf, thbuf, broadcast: bool, batch: int, seed: int, offset: int = 0):
+        """df_flow_sample: device N(0, I) draw (Philox, seed/offset) + fused forward!."""
+        _lib.check(self.lib.df_flow_sample(self.handle, _ptr(xbuf), _ptr(thbuf), 1 if broadcast else 0,
+                                           C.c_int64(batch), C.c_uint64(seed), C.c_uint64(offset),
+                                           _stream(self.device)), "sample")
+
+    def random_normal(self, buf, count: int, seed: int, offset: int = 0):
+        """df_random_normal: the draw df_flow_sample uses for the same (seed, offset)."""
+        _lib.check(self.lib.df_random_normal(_ptr(buf), C.c_int64(count), C.c_uint64(seed), C.c_uint64(offset),
+                                             _stream(self.device)), "random_normal")
+
     # -- array-level API ---------------------------------------------------
     def _inputs(self, y, theta, name):
         yb, dims, was_np = as_julia_device(y, self.d, self.device, name)

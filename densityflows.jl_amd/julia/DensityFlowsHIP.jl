@@ -13,10 +13,12 @@ so `Flow`'s @flow_wrapper methods (src/Macros.jl:104-112), `logpdf`
 (src/Flows.jl:272-281) and `sample` (src/Flows.jl:157-192) run on the MI355X
 unchanged once the chain is wrapped: `FlowChain((HIPFlowChain(chain),))`.
 
-STATUS: written against include/densityflows_hip.h (ABI 1) but NOT executed —
-there is no Julia toolchain in this build pipeline (SURVEY.md §8c).  The same
-entry points are exercised from Python (densityflows.jl_amd/_lib.py) by the
-parity tests.
+STATUS: written against include/densityflows_hip.h (ABI 3; `__init__` refuses a
+library of another ABI) but NOT executed — there is no Julia toolchain in this
+build pipeline (SURVEY.md §8c).  The same entry points are exercised from
+Python (densityflows.jl_amd/_lib.py) by the parity tests, and
+tests/test_julia_shim.py checks this file's method signatures statically
+against the reference's (dispatch specificity, AbstractArray inputs).
 
 Host `Array{Float32}` arguments are staged through device buffers
 (df_device_alloc / df_memcpy_*); device arrays (AMDGPU.jl `ROCArray`) can be
@@ -25,16 +27,21 @@ passed by pointer to the same entry points without copies.
 module DensityFlowsHIP
 
 using DensityFlows
-import DensityFlows: forward, backward, forward!, train!, FlowElement, CouplingLayer, CouplingBlock,
+import DensityFlows: forward, backward, forward!, train!, sample, FlowElement, CouplingLayer, CouplingBlock,
                      FlowChain, RNVPCouplingLayer, NICECouplingLayer, NormalizationLayer, Flow, DataArrays
-import Distributions, LinearAlgebra
+import Distributions, LinearAlgebra, Random
 import Flux, Optimisers
 
 export HIPFlowChain, HIPTrainer, HIPComm, train_step!, train_step_graph!, train_step_dist!, trainables,
-       copy_trainables!, hip_flow, flow_nll
+       copy_trainables!, hip_flow, flow_nll, sample
 
 const LIB = get(ENV, "DENSITYFLOWS_HIP_LIB", joinpath(@__DIR__, "..", "libdensityflows_hip.so"))
-const ABI_VERSION = Int32(2)
+const ABI_VERSION = Int32(3)
+
+function __init__()
+    v = ccall((:df_get_abi_version, LIB), Cint, ())
+    v == ABI_VERSION || error("$LIB has ABI version $v, this binding needs $ABI_VERSION")
+end
 
 # ---- C structs (include/densityflows_hip.h) --------------------------------
 struct DenseDesc                 # df_dense_desc
@@ -108,7 +115,15 @@ mutable struct HIPFlowChain <: FlowElement
     n::Int
     keep::Vector{Any}               # host arrays the descriptor pointed to (until create returns)
     stage::Staging                  # [y, θ, out, ldj, Σ]
+    params::Vector{Float32}         # host copy of the trainables (Flux.trainables order): what
+                                    # Optimisers.setup sees, so the rule it wraps reaches train!
+    trainer::Any                    # the device trainer of this chain (Nothing or HIPTrainer)
+    trainer_key::Any                # its Adam hyper-parameters
+    bounds::Any                     # θ bounds last given to df_chain_set_theta_bounds
 end
+
+# Optimisers.setup(rule, FlowChain((HIPFlowChain(chain),))) yields a Leaf holding `rule`
+Optimisers.trainable(c::HIPFlowChain) = (; params = c.params)
 
 # flatten the chain into (element index, layer) pairs; blocks share an element
 function _flatten(chain::FlowChain)
@@ -170,9 +185,12 @@ function HIPFlowChain(chain::FlowChain; device::Integer = 0)
         check(ccall((:df_chain_create, LIB), Cint, (Ptr{Ptr{Cvoid}}, Ref{ChainDesc}, Cint),
                     h, desc, device), "df_chain_create")
     end
-    obj = HIPFlowChain(h[], d, max(n, 0), Any[], Staging(5))
+    params = isempty(Flux.trainables(chain)) ? Float32[] :
+             reduce(vcat, [vec(Float32.(a)) for a in Flux.trainables(chain)])
+    obj = HIPFlowChain(h[], d, max(n, 0), Any[], Staging(5), params, nothing, nothing, nothing)
     finalizer(obj) do c
         _release!(c.stage)
+        c.trainer === nothing || _destroy!(c.trainer)   # df_chain_destroy needs its trainers gone
         ccall((:df_chain_destroy, LIB), Cint, (Ptr{Cvoid},), c.handle)
     end
     return obj
@@ -190,7 +208,13 @@ _h2d(dst, src::Array) = check(ccall((:df_memcpy_h2d, LIB), Cint, (Ptr{Cvoid}, Pt
 _d2h(dst::Array, src) = check(ccall((:df_memcpy_d2h, LIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
                                     dst, src, sizeof(dst), C_NULL), "d2h")
 
-function _run(sym::Symbol, c::HIPFlowChain, y::Array{Float32,N}, θ::Array{Float32,N}) where {N}
+# device calls take contiguous column-major arrays; views (selectdim in
+# normalized_training_data, src/Data.jl:185-193) are copied first
+_dense(a::Array{Float32}) = a
+_dense(a::AbstractArray{Float32}) = Array{Float32}(a)
+
+function _run(sym::Symbol, c::HIPFlowChain, y::AbstractArray{Float32,N}, θ::AbstractArray{Float32,N}) where {N}
+    y, θ = _dense(y), _dense(θ)
     @assert size(y, 1) == c.d "input must be (d, dims...)"
     @assert size(θ, 1) == c.n "dimensions θ must match (n, dims...) with n number of trained parameters"
     B = prod(size(y)[2:N])
@@ -204,26 +228,31 @@ function _run(sym::Symbol, c::HIPFlowChain, y::Array{Float32,N}, θ::Array{Float
     return out, ldj
 end
 
-forward(c::HIPFlowChain, z::Array{Float32,N}, θ::Array{Float32,N}) where {N} = _run(:df_chain_forward, c, z, θ)
-backward(c::HIPFlowChain, x::Array{Float32,N}, θ::Array{Float32,N}) where {N} = _run(:df_chain_backward, c, x, θ)
+forward(c::HIPFlowChain, z::AbstractArray{Float32,N}, θ::AbstractArray{Float32,N}) where {N} =
+    _run(:df_chain_forward, c, z, θ)
+backward(c::HIPFlowChain, x::AbstractArray{Float32,N}, θ::AbstractArray{Float32,N}) where {N} =
+    _run(:df_chain_backward, c, x, θ)
 
 """forward!(c, z, θ): src/Chains.jl:187-197 — z overwritten by the chain's output
 (df_chain_forward_inplace: one staging buffer, no ldj)."""
-function forward!(c::HIPFlowChain, z::Array{Float32,N}, θ::Array{Float32,N}) where {N}
+function forward!(c::HIPFlowChain, z::AbstractArray{Float32,N}, θ::AbstractArray{Float32,N}) where {N}
+    zz, θ = _dense(z), _dense(θ)
     @assert size(z, 1) == c.d "input must be (d, dims...)"
     @assert size(θ, 1) == c.n "dimensions θ must match (n, dims...) with n number of trained parameters"
     B = prod(size(z)[2:N])
-    dz, dθ = _buf!(c.stage, 1, sizeof(z)), _buf!(c.stage, 2, sizeof(θ))
-    _h2d(dz, z); c.n > 0 && _h2d(dθ, θ)
+    dz, dθ = _buf!(c.stage, 1, sizeof(zz)), _buf!(c.stage, 2, sizeof(θ))
+    _h2d(dz, zz); c.n > 0 && _h2d(dθ, θ)
     check(ccall((:df_chain_forward_inplace, LIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
                 c.handle, dz, c.n > 0 ? dθ : C_NULL, B, C_NULL), "df_chain_forward_inplace")
-    _d2h(z, dz)
+    _d2h(zz, dz)
+    zz === z || copyto!(z, zz)
     return nothing
 end
 
 """Σ_j logpdf_j (fp64, on the device) of the chain's inverse pass under MvNormal(0, I):
 the sum src/Flows.jl:352-359 averages.  θ as given (already normalised)."""
-function logpdf_sum(c::HIPFlowChain, x::Array{Float32,N}, θ::Array{Float32,N}) where {N}
+function logpdf_sum(c::HIPFlowChain, x::AbstractArray{Float32,N}, θ::AbstractArray{Float32,N}) where {N}
+    x, θ = _dense(x), _dense(θ)
     B = prod(size(x)[2:N])
     dx, dθ, ds = _buf!(c.stage, 1, sizeof(x)), _buf!(c.stage, 2, sizeof(θ)), _buf!(c.stage, 5, 16)
     _h2d(dx, x); c.n > 0 && _h2d(dθ, θ)
@@ -249,6 +278,14 @@ mutable struct HIPTrainer
     stage::Staging                  # [x, θ, Σ logpdf]
 end
 
+function _destroy!(t::HIPTrainer)
+    t.handle == C_NULL && return nothing
+    _release!(t.stage)
+    ccall((:df_train_destroy, LIB), Cint, (Ptr{Cvoid},), t.handle)
+    t.handle = C_NULL
+    return nothing
+end
+
 """Optimisers.setup(Adam(η, β, ϵ), model) on the device; the trainer owns the flat trainables."""
 function HIPTrainer(c::HIPFlowChain; eta=1f-3, beta=(0.9f0, 0.999f0), epsilon=1f-8)
     t = Ref{Ptr{Cvoid}}(C_NULL)
@@ -257,16 +294,14 @@ function HIPTrainer(c::HIPFlowChain; eta=1f-3, beta=(0.9f0, 0.999f0), epsilon=1f
     n = Ref{Int64}(0)
     check(ccall((:df_train_num_params, LIB), Cint, (Ptr{Cvoid}, Ref{Int64}), t[], n), "df_train_num_params")
     obj = HIPTrainer(t[], c, n[], Staging(3))
-    finalizer(obj) do x
-        _release!(x.stage)
-        ccall((:df_train_destroy, LIB), Cint, (Ptr{Cvoid},), x.handle)
-    end
+    finalizer(_destroy!, obj)
     return obj
 end
 
 """One mini-batch step of train! (gradient of loss(backward(m, x, θ)) + Adam update).
 Returns the batch loss before the update (−Σ logpdf / B)."""
-function train_step!(t::HIPTrainer, x::Array{Float32,N}, θ::Array{Float32,N}) where {N}
+function train_step!(t::HIPTrainer, x::AbstractArray{Float32,N}, θ::AbstractArray{Float32,N}) where {N}
+    x, θ = _dense(x), _dense(θ)
     B = prod(size(x)[2:N])
     dx, dθ, ds = _buf!(t.stage, 1, sizeof(x)), _buf!(t.stage, 2, sizeof(θ)), _buf!(t.stage, 3, 8)
     _h2d(dx, x); t.chain.n > 0 && _h2d(dθ, θ)
@@ -354,8 +389,9 @@ Config 3's sharded NLL, `loss = -mean(logpdf)` (src/Flows.jl:352-359) over the
 union of every rank's shard: df_flow_nll all-reduces {Σ logpdf, N} over RCCL.
 θ as given (already normalised).  `comm = nothing`: this process only.
 """
-function flow_nll(c::HIPFlowChain, comm::Union{HIPComm,Nothing}, x::Array{Float32,N},
-                  θ::Array{Float32,N}) where {N}
+function flow_nll(c::HIPFlowChain, comm::Union{HIPComm,Nothing}, x::AbstractArray{Float32,N},
+                  θ::AbstractArray{Float32,N}) where {N}
+    x, θ = _dense(x), _dense(θ)
     B = prod(size(x)[2:N])
     dx, dθ, ds = _buf!(c.stage, 1, sizeof(x)), _buf!(c.stage, 2, sizeof(θ)), _buf!(c.stage, 5, 16)
     _h2d(dx, x); c.n > 0 && _h2d(dθ, θ)
@@ -375,8 +411,9 @@ One data-parallel train! step: this rank's gradient with the mean over the globa
 batch `n_total`, RCCL all-reduce of ∇ and Σ logpdf, the identical Adam step on
 every rank (df_train_step_dist).  Returns the global batch loss before the update.
 """
-function train_step_dist!(t::HIPTrainer, comm::HIPComm, x::Array{Float32,N}, θ::Array{Float32,N},
+function train_step_dist!(t::HIPTrainer, comm::HIPComm, x::AbstractArray{Float32,N}, θ::AbstractArray{Float32,N},
                           n_total::Integer) where {N}
+    x, θ = _dense(x), _dense(θ)
     B = prod(size(x)[2:N])
     dx, dθ, ds = _buf!(t.stage, 1, sizeof(x)), _buf!(t.stage, 2, sizeof(θ)), _buf!(t.stage, 3, 8)
     _h2d(dx, x); t.chain.n > 0 && _h2d(dθ, θ)
@@ -398,24 +435,31 @@ _adam(rule::Optimisers.Adam) = (Float32(rule.eta), (Float32(rule.beta[1]), Float
                                 Float32(rule.epsilon))
 _adam(::Any) = throw(ArgumentError("the device optimiser is Optimisers.Adam"))
 
-function _trainer!(flow::Flow, opt)
-    c = flow.model.layers[1]
-    opt isa HIPTrainer && (opt.chain === c || throw(ArgumentError("trainer of another chain")); return opt)
-    # Optimisers.setup(Adam(η, β, ϵ), flow.model): the rule is the state's only content
-    # the device needs; the trainer (and its moments) lives as long as the chain
-    rule = opt isa Optimisers.AbstractRule ? opt : _state_rule(opt)
+# The device trainer of a chain lives on the chain (created on first use, replaced when
+# the Adam hyper-parameters change), so its lifetime — and its device moments — follow
+# the chain's; the chain's finalizer destroys it first.
+function _trainer!(c::HIPFlowChain, rule)
     η, β, ϵ = _adam(rule)
     key = (η, β, ϵ)
-    t = get!(() -> HIPTrainer(c; eta = η, beta = β, epsilon = ϵ), _TRAINERS, (objectid(c), key))
-    return t
+    if c.trainer === nothing || c.trainer_key != key
+        c.trainer === nothing || _destroy!(c.trainer)
+        c.trainer = HIPTrainer(c; eta = η, beta = β, epsilon = ϵ)
+        c.trainer_key = key
+    end
+    return c.trainer
 end
-const _TRAINERS = IdDict{Any,HIPTrainer}()
 
+# The rule inside Optimisers.setup(rule, flow.model): HIPFlowChain exposes its flat
+# trainables (Optimisers.trainable), so the state tree holds one Leaf with the user's
+# rule.  A state without a Leaf was not built from this model: refuse it.
 function _state_rule(state)
-    leaf = nothing
-    Optimisers.fmap(x -> (x isa Optimisers.Leaf && (leaf = x); x), state; exclude = x -> x isa Optimisers.Leaf)
-    leaf === nothing && return Optimisers.Adam()        # setup() of a HIP-wrapped model has no leaves
-    return leaf.rule
+    rules = Any[]
+    Optimisers.fmap(x -> (x isa Optimisers.Leaf && push!(rules, x.rule); x), state;
+                    exclude = x -> x isa Optimisers.Leaf)
+    isempty(rules) && throw(ArgumentError("optimiser state holds no Optimisers.Leaf: build it with " *
+                                          "Optimisers.setup(Adam(η), flow.model) on the HIP-wrapped model"))
+    all(r -> r == rules[1], rules) || throw(ArgumentError("one Adam rule per HIP chain"))
+    return rules[1]
 end
 
 """
@@ -432,13 +476,33 @@ before the update (as the reference); a NaN/Inf epoch loss prints and returns
 `(z, ldj)` of that set; returns `(nothing, nothing)` at the end.
 Copy the trained parameters into a Julia model with `copy_trainables!`.
 """
-function train!(flow::Flow{T,D,N,<:HIPModel}, data::DataArrays{T}, opt; epochs::Int = 100,
-                batchsize::Int = 64, shuffle::Bool = true, verbose::Bool = true, debug::Bool = false) where {T,D,N}
+# The reference method is train!(flow::Flow{T}, data::DataArrays{T}, optimiser_state::NamedTuple; ...)
+# (src/Flows.jl:380-389).  This one is strictly more specific (argument 1 narrower, the
+# others equal), so the reference's own call `train!(flow, data, Optimisers.setup(Adam(η),
+# flow.model))` dispatches here without ambiguity.
+function train!(flow::Flow{T,D,N,<:HIPModel}, data::DataArrays{T}, optimiser_state::NamedTuple;
+                kws...) where {T,D,N}
+    c = flow.model.layers[1]
+    return _hip_train!(flow, data, _trainer!(c, _state_rule(optimiser_state)); kws...)
+end
+
+# An Optimisers rule or a HIPTrainer directly (argument 3 disjoint from NamedTuple: no
+# ambiguity with the reference method).
+train!(flow::Flow{T,D,N,<:HIPModel}, data::DataArrays{T}, rule::Optimisers.AbstractRule; kws...) where {T,D,N} =
+    _hip_train!(flow, data, _trainer!(flow.model.layers[1], rule); kws...)
+
+function train!(flow::Flow{T,D,N,<:HIPModel}, data::DataArrays{T}, t::HIPTrainer; kws...) where {T,D,N}
+    t.chain === flow.model.layers[1] || throw(ArgumentError("trainer of another chain"))
+    return _hip_train!(flow, data, t; kws...)
+end
+
+function _hip_train!(flow::Flow{T,D,N}, data::DataArrays{T}, t::HIPTrainer; epochs::Int = 100,
+                     batchsize::Int = 64, shuffle::Bool = true, verbose::Bool = true,
+                     debug::Bool = false) where {T,D,N}
     flow.base isa Distributions.MvNormal && all(iszero, Distributions.mean(flow.base)) &&
         Distributions.cov(flow.base) == LinearAlgebra.diagm(ones(T, D)) ||
         throw(ArgumentError("the device loss is the MvNormal(0, I) base of Flow(model, data)"))
     c = flow.model.layers[1]
-    t = _trainer!(flow, opt)
     set_debug!(t, debug)
     train_data = DensityFlows.normalized_training_data(data, flow.metadata)
     valid_data = DensityFlows.normalized_validation_data(data, flow.metadata)
@@ -450,6 +514,7 @@ function train!(flow::Flow{T,D,N,<:HIPModel}, data::DataArrays{T}, opt; epochs::
                 train_step!(t, x_batch, t_batch)
             catch e
                 e isa NonFiniteLoss || rethrow()
+                copyto!(c.params, trainables(t))   # the last good parameters, as update! left them
                 z, ldj = backward(c, x_batch, t_batch)
                 println("$(e.loss), $ldj, $z")
                 throw(ArgumentError(""))
@@ -459,19 +524,65 @@ function train!(flow::Flow{T,D,N,<:HIPModel}, data::DataArrays{T}, opt; epochs::
         push!(flow.train_loss, train_loss)
         if debug && ((train_loss != train_loss) || isinf(train_loss))
             println("Problem with train loss $train_loss")
+            copyto!(c.params, trainables(t))
             return backward(c, train_data...)
         end
         valid_loss = setloss(valid_data)
         push!(flow.valid_loss, valid_loss)
         if debug && ((valid_loss != valid_loss) || isinf(valid_loss))
             println("Problem with valid loss $valid_loss")
+            copyto!(c.params, trainables(t))
             return backward(c, valid_data...)
         end
         verbose && println("epoch: $(length(flow.train_loss)) | train_loss = $train_loss, valid_loss = $valid_loss")
     end
+    copyto!(c.params, trainables(t))               # host mirror of the trained parameters
     debug && return nothing, nothing
     return nothing
 end
+
+# ---- sample (src/Flows.jl:157-192) on the device ----------------------------------
+function _set_bounds!(c::HIPFlowChain, md)
+    c.n == 0 && return nothing
+    b = (Vector{Float32}(md.θ_min), Vector{Float32}(md.θ_max))
+    c.bounds == b && return nothing
+    check(ccall((:df_chain_set_theta_bounds, LIB), Cint, (Ptr{Cvoid}, Ptr{Float32}, Ptr{Float32}),
+                c.handle, b[1], b[2]), "df_chain_set_theta_bounds")
+    c.bounds = b
+    return nothing
+end
+
+# r ~ MvNormal(0, I) drawn on the device (Philox4x32-10 keyed by 64 bits of `rng`, so a
+# seeded rng reproduces the sample; Julia's own Xoshiro stream is not reproduced), then
+# forward!(flow, r, θ) with θ normalised in the kernel: one df_flow_sample call.
+function _hip_sample(rng::Random.AbstractRNG, flow::Flow, dims::Tuple, θ::Array{Float32}, bcast::Bool)
+    c = flow.model.layers[1]
+    _set_bounds!(c, flow.metadata)
+    B = prod(dims)
+    r = Array{Float32}(undef, c.d, dims...)
+    dr, dθ = _buf!(c.stage, 3, sizeof(r)), _buf!(c.stage, 2, sizeof(θ))
+    c.n > 0 && _h2d(dθ, θ)
+    check(ccall((:df_flow_sample, LIB), Cint,
+                (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Cint, Int64, UInt64, UInt64, Ptr{Cvoid}),
+                c.handle, dr, c.n > 0 ? dθ : C_NULL, bcast ? 1 : 0, B, rand(rng, UInt64), 0, C_NULL),
+          "df_flow_sample")
+    _d2h(r, dr)
+    return r
+end
+
+# The reference methods are sample(rng, flow::Flow{T,D}, dims::NTuple{M,Integer},
+# θ::AbstractArray{T,K}) and sample(rng, flow::Flow{T,D,N}, dims::Tuple{Vararg{Integer}},
+# θ::NTuple{N,T}) (src/Flows.jl:159-188); these narrow argument 2 only, and the
+# convenience methods (Integer dims, default rng, :190-195) dispatch to them.
+function sample(rng::Random.AbstractRNG, flow::Flow{T,D,N,<:HIPModel}, dims::NTuple{M,Integer},
+                θ::AbstractArray{T,K} = DensityFlows.dflt_θ(T, dims)) where {T,D,N,M,K}
+    @assert K == M + 1 "dimensions θ must match (n, dims...) with n number of trained parameters"
+    @assert size(θ, 1) == N && size(θ)[2:end] == Tuple(dims) "dimensions θ must match (n, dims...) with n number of trained parameters"
+    return _hip_sample(rng, flow, Tuple(dims), _dense(Float32.(θ)), false)
+end
+
+sample(rng::Random.AbstractRNG, flow::Flow{T,D,N,<:HIPModel}, dims::Tuple{Vararg{Integer}},
+       θ::NTuple{N,T}) where {T,D,N} = _hip_sample(rng, flow, Tuple(dims), Float32[θ...], true)
 
 """
     copy_trainables!(model::FlowChain, p::Vector{Float32})

@@ -310,6 +310,16 @@ def train_(flow, data, state: TrainState, epochs: int = 100, batchsize: int = 64
                             raise _lib.NonFiniteError(f"non-finite training loss {-float(lp.item()) / B}")
                     tr.apply()
             except _lib.NonFiniteError as e:
+                # the reference throws from inside the gradient closure, after printing
+                # "$l, $ln_det_jac, $z" of the batch (src/Flows.jl:404-409); update! has
+                # left flow.model at the last good parameters, and so does sync_model here
+                state.sync_model()
+                if rank == 0:
+                    xv = xb[: b - a].T if local and graphs else xb.T
+                    tv = (tb[: b - a].T if local and graphs else tb.T) if tb is not None else None
+                    z, ldj = flow.backward(xv, tv)
+                    s = flow.hip().logpdf_sum(xv, tv)[0]
+                    print(f"{-float(s.item()) / max(b - a, 1)}, {ldj.cpu().numpy()}, {z.cpu().numpy()}")
                 raise _lib.ArgumentError(str(e)) from e
         train_loss = _loss(flow, x_tr, th_tr if n > 0 else None, group, comm)
         flow.train_loss.append(train_loss)

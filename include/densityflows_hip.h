@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DF_ABI_VERSION 2
+#define DF_ABI_VERSION 3
 
 typedef enum df_status {
     DF_OK = 0,
@@ -197,6 +197,22 @@ int df_flow_logpdf(df_chain* chain, const float* x, const float* theta_raw,
                    float* logpdf_out, int64_t batch, void* stream);
 int df_flow_logpdf_sum(df_chain* chain, const float* x, const float* theta_raw,
                        double* sum_out, int64_t batch, void* stream);
+
+/* ---- sampling ---------------------------------------------------------------
+ * sample(flow, dims, θ) (src/Flows.jl:157-192): r ~ MvNormal(0, I) (Flows.jl:114)
+ * drawn on the device, then forward!(flow, r, θ) — df_flow_forward_inplace, θ raw and
+ * normalised in the kernel with the chain's bounds.  x_out: (d, batch) device memory;
+ * for dims = (d1, d2, ...) pass batch = prod(dims) (the column-major (d, dims...) array
+ * is the (d, batch) one).  theta_broadcast = 0: theta_raw is (n, batch); 1: theta_raw
+ * is ONE n-vector used for every sample (the NTuple θ method, Flows.jl:178-188).
+ * The draw: element k of the (d, batch) array comes from Philox4x32-10 with key =
+ * seed and counter (offset + k/4, 0, 0, 0), word k%4; words (0,1), (2,3) are
+ * Box-Muller pairs.  Julia's Xoshiro stream is not reproduced (by design);
+ * df_random_normal returns the same draw on its own, so a caller can check
+ * forward!(draw) against df_flow_sample with the same (seed, offset). */
+int df_flow_sample(df_chain* chain, float* x_out, const float* theta_raw, int theta_broadcast, int64_t batch,
+                   uint64_t seed, uint64_t offset, void* stream);
+int df_random_normal(float* out, int64_t count, uint64_t seed, uint64_t offset, void* stream);
 
 /* ---- training ---------------------------------------------------------------
  * train!(flow, data, opt_state; ...) src/Flows.jl:380-445: per batch

@@ -24,14 +24,14 @@ def build(rng_seed=0):
     return data, chain, dfa.Flow(chain, data)
 
 
-def run(group=None, epochs=2):
+def run(group=None, epochs=2, comm=None, graphs=True):
     import densityflows_amd as dfa
     from densityflows_amd.train import trainables
 
     data, chain, flow = build()
     state = dfa.setup(dfa.Adam(1e-3), flow)
     dfa.train_(flow, data, state, epochs=epochs, batchsize=64, verbose=False, rng=np.random.default_rng(1),
-               group=group)
+               group=group, comm=comm, graphs=graphs)
     return trainables(chain), np.asarray(flow.train_loss), np.asarray(flow.valid_loss)
 
 
@@ -39,9 +39,20 @@ if __name__ == "__main__":
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(0)  # rehearsal: every rank shares GPU 0
+    rccl = len(sys.argv) > 2 and sys.argv[2] == "rccl"
+    rank = int(os.environ["RANK"])
+    comm = None
+    # gloo carries the bootstrap (and, in the rehearsal, the gradient); with "rccl" every
+    # rank owns its GPU and the library's communicator carries every exchange
+    torch.cuda.set_device(rank if rccl else 0)
     dist.init_process_group("gloo")
-    p, tl, vl = run()
+    if rccl:
+        from densityflows_amd.parallel import DFComm
+
+        comm = DFComm(rank, rank, dist.get_world_size())
+    p, tl, vl = run(comm=comm)
+    if comm is not None:
+        comm.close()
     if dist.get_rank() == 0:
         np.savez(sys.argv[1], params=p, train_loss=tl, valid_loss=vl)
     dist.barrier()

@@ -117,3 +117,47 @@ def test_two_rank_sharded_nll_gloo(cuda, tmp_path):
     # the shard partial is the fp64 sum of the golden logpdf over rank 0's half
     half = g["logpdf"][: meta["B"] // 2].astype(np.float64)
     assert abs(float(res["shard_sum"]) - half.sum()) <= 1e-5 * np.abs(half).sum()
+
+
+def test_world1_train_with_comm_matches_local(cuda, comm):
+    """train_(..., comm=DFComm) — df_train_step_dist per mini-batch, df_flow_nll per
+    epoch — through a real world-1 RCCL communicator equals the local train_ bitwise:
+    parameters and the train / valid loss vectors (src/Flows.jl:380-445)."""
+    import dist_train_worker as W
+
+    local = W.run(graphs=False)
+    dist = W.run(comm=comm)
+    np.testing.assert_array_equal(local[0], dist[0])
+    np.testing.assert_array_equal(local[1], dist[1])
+    np.testing.assert_array_equal(local[2], dist[2])
+
+
+def test_two_rank_rccl_train(cuda, tmp_path):
+    """Two ranks, one GPU each, the library's RCCL communicator for every exchange
+    (gradient all-reduce, {Σ, N} of the epoch losses): the data-parallel train_ matches
+    one process on the same batches to the gradient tolerance (the shard sums
+    reassociate the batch mean).  Needs two GPUs."""
+    import torch
+
+    import dist_train_worker as W
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (one rank per GPU)")
+    out = str(tmp_path / "rccl_train.npz")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.join(os.path.dirname(__file__), "dist_train_worker.py"), out, "rccl"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = np.load(out)
+    p1, tl1, vl1 = W.run()
+    np.testing.assert_allclose(res["train_loss"], tl1, rtol=1e-4)
+    np.testing.assert_allclose(res["valid_loss"], vl1, rtol=1e-4)
+    # as the gloo rehearsal (test_gpu_train.py): Adam normalises each step to ≈ η, so
+    # reassociated gradient sums move near-zero-gradient coordinates by O(η)
+    assert np.max(np.abs(res["params"] - p1)) <= 2e-3
+    assert np.mean(np.abs(res["params"] - p1)) <= 2e-5

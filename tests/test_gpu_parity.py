@@ -395,12 +395,11 @@ def test_flow_forward_inplace_theta_tuple_and_normalization(cuda):
 
 @pytest.mark.parametrize("theta", ["array", "tuple"])
 def test_sample_values_against_oracle(cuda, theta):
-    """sample(flow, dims, θ) with a seeded device generator: the same draw r,
-    replayed from the same seed, through O.forward_inplace (src/Flows.jl:174-185;
-    Julia's Xoshiro stream itself cannot be matched)."""
+    """sample(flow, dims, θ) through df_flow_sample (device Philox draw + fused
+    forward!): the same draw read back with df_random_normal (same seed) through
+    O.forward_inplace (src/Flows.jl:174-185; Julia's Xoshiro stream itself cannot be
+    matched), and bitwise the library's own forward! of that draw."""
     import torch
-
-    from densityflows_amd.hip import julia_empty
 
     spec, g, meta = G.load("cfg1")
     flow = dfa.Flow(spec_to_element(spec), metadata=dfa.MetaData("", 5, 1, g["theta_min"], g["theta_max"]))
@@ -411,14 +410,47 @@ def test_sample_values_against_oracle(cuda, theta):
     else:
         th_raw = np.random.default_rng(3).uniform(-1, 2, (1, B)).astype(np.float32)
         th_arg = th_raw.reshape((1,) + dims, order="F")     # logical (n, dims...), Julia memory order
-    s = dfa.sample(flow, dims, th_arg, generator=torch.Generator(device=cuda).manual_seed(77))
-    buf, r = julia_empty(5, dims, cuda)
-    buf.normal_(0.0, 1.0, generator=torch.Generator(device=cuda).manual_seed(77))
-    rn = _np(r).reshape(5, B, order="F").astype(np.float64)
+    s = dfa.sample(flow, dims, th_arg, seed=77)
+    buf = torch.empty(5 * B, dtype=torch.float32, device=cuda)
+    flow.hip().random_normal(buf, 5 * B, 77)
+    rn = _np(buf).reshape(5, B, order="F").astype(np.float64)
+    r2 = buf.reshape(B, 5).T                                 # logical (5, B) view, Julia order
+    flow.forward_(r2, _t(th_raw, cuda))
     O.forward_inplace(spec, rn, O.normalize_input(th_raw, g["theta_min"], g["theta_max"]), np.float64)
     assert tuple(s.shape) == (5,) + dims
-    ok, rr = close(_np(s).reshape(5, B, order="F"), rn, RTOL)
+    sv = _np(s).reshape(5, B, order="F")
+    ok, rr = close(sv, rn, RTOL)
     assert ok, rr
+    np.testing.assert_array_equal(sv, _np(r2))
+
+
+def test_device_normal_draw_moments(cuda):
+    """df_random_normal (the base draw of df_flow_sample, MvNormal(0, I) of
+    src/Flows.jl:114): moments of 2^22 draws, determinism in (seed, offset), and a
+    different stream for another seed or offset."""
+    import torch
+
+    spec, g, meta = G.load("cfg1")
+    h = spec_to_element(spec).hip()
+    N = 1 << 22
+    a = torch.empty(N, dtype=torch.float32, device=cuda)
+    b = torch.empty(N, dtype=torch.float32, device=cuda)
+    h.random_normal(a, N, 12345)
+    z = _np(a).astype(np.float64)
+    assert np.all(np.isfinite(z))
+    assert abs(z.mean()) < 3e-3 and abs(z.var() - 1.0) < 3e-3
+    assert abs(np.mean(z ** 4) - 3.0) < 3e-2                     # kurtosis of N(0, 1)
+    assert abs(np.mean(np.abs(z) < 1.0) - 0.682689) < 2e-3
+    assert abs(np.mean(np.abs(z) < 2.0) - 0.954500) < 1e-3
+    h.random_normal(b, N, 12345)
+    np.testing.assert_array_equal(_np(a), _np(b))
+    h.random_normal(b, N, 12346)
+    assert np.mean(_np(a) == _np(b)) < 1e-3
+    h.random_normal(b, N - 4, 12345, offset=1)                   # counter offset: the stream shifted by 4
+    np.testing.assert_array_equal(_np(a)[4:], _np(b)[:N - 4])
+    # ragged counts: the draw of a prefix is the prefix of the draw
+    h.random_normal(b, 1001, 12345)
+    np.testing.assert_array_equal(_np(a)[:1001], _np(b)[:1001])
 
 
 def test_theta_row_with_max_equal_min(cuda):

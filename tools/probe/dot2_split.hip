@@ -101,6 +101,31 @@ __global__ void k_planes(uint32_t seed, int pass, uint32_t* out) {
     out[3 * i + 2] = w[2];
 }
 
+// The matrix-pipe remainders (df::uni::split8_mrem, DF_SPLIT_MREM): each lane's 8
+// values as two accumulator tiles, planes written per pair in the k_planes layout.
+// Non-finite inputs are zeroed first (0·inf in the −I product would poison the column;
+// such activations have overflowed already), and their planes reported as 0.
+__global__ void k_planes_mrem(uint32_t seed, int pass, uint32_t* out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    float v[8];
+    bool sk[4];
+    for (int q = 0; q < 4; ++q) {
+        float x0, x1;
+        probe_inputs(4 * t + q, seed, pass, x0, x1, sk[q]);
+        v[2 * q] = sk[q] ? 0.f : x0;
+        v[2 * q + 1] = sk[q] ? 0.f : x1;
+    }
+    const df::f32x4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
+    df::uni::bf16x8 p[3];
+    df::uni::split8_mrem(df::uni::neg_eye(), a, b, p[0], p[1], p[2]);
+    for (int q = 0; q < 4; ++q)
+        for (int pl = 0; pl < 3; ++pl) {
+            const uint32_t w = (uint32_t)__builtin_bit_cast(uint16_t, p[pl][2 * q]) |
+                               (uint32_t)__builtin_bit_cast(uint16_t, p[pl][2 * q + 1]) << 16;
+            out[3 * (4 * t + q) + pl] = sk[q] ? 0u : w;
+        }
+}
+
 int main() {
     unsigned long long* bad;
     uint32_t* ex;
@@ -139,6 +164,20 @@ int main() {
             if (memcmp(hh + 3 * i, hp + 3 * i, 12) != 0) { if (!bad_pairs) first = i; ++bad_pairs; }
         printf("split2 helper %-28s mismatches %zu of 2^24", names[pass], bad_pairs);
         if (bad_pairs) printf("  e.g. pair %zu: helper %08x %08x %08x plain %08x %08x %08x", first, hh[3 * first],
+                              hh[3 * first + 1], hh[3 * first + 2], hp[3 * first], hp[3 * first + 1], hp[3 * first + 2]);
+        printf("\n");
+        if (bad_pairs) rc = 1;
+    }
+    for (int pass = 0; pass < 4; ++pass) {   // the matrix-pipe form against the plain split
+        hipLaunchKernelGGL(k_planes_mrem, dim3(np / 4 / 256), dim3(256), 0, 0, 1234u + pass, pass, dh);
+        hipLaunchKernelGGL(k_planes<0>, dim3(np / 256), dim3(256), 0, 0, 1234u + pass, pass, dp);
+        hipMemcpy(hh, dh, nb, hipMemcpyDeviceToHost);
+        hipMemcpy(hp, dp, nb, hipMemcpyDeviceToHost);
+        size_t bad_pairs = 0, first = 0;
+        for (size_t i = 0; i < np; ++i)
+            if (memcmp(hh + 3 * i, hp + 3 * i, 12) != 0) { if (!bad_pairs) first = i; ++bad_pairs; }
+        printf("split8 mrem   %-28s mismatches %zu of 2^24", names[pass], bad_pairs);
+        if (bad_pairs) printf("  e.g. pair %zu: mrem %08x %08x %08x plain %08x %08x %08x", first, hh[3 * first],
                               hh[3 * first + 1], hh[3 * first + 2], hp[3 * first], hp[3 * first + 1], hp[3 * first + 2]);
         printf("\n");
         if (bad_pairs) rc = 1;
