@@ -118,12 +118,13 @@ __global__ void k_planes_mrem(uint32_t seed, int pass, uint32_t* out) {
     const df::f32x4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
     df::uni::bf16x8 p[3];
     df::uni::split8_mrem(df::uni::neg_eye(), a, b, p[0], p[1], p[2]);
-    for (int q = 0; q < 4; ++q)
-        for (int pl = 0; pl < 3; ++pl) {
-            const uint32_t w = (uint32_t)__builtin_bit_cast(uint16_t, p[pl][2 * q]) |
-                               (uint32_t)__builtin_bit_cast(uint16_t, p[pl][2 * q + 1]) << 16;
-            out[3 * (4 * t + q) + pl] = sk[q] ? 0u : w;
-        }
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+        const u32x4 w = __builtin_bit_cast(u32x4, p[pl]);   // dword q = elements (2q, 2q+1)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[3 * (4 * t + q) + pl] = sk[q] ? 0u : w[q];
+    }
 }
 
 int main() {
