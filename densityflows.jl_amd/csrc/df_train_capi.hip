@@ -275,7 +275,6 @@ int build_lnets(df_train* t) {
                 if (k + 1 < nd && act_needs_pre(D.act)) net.pre = true;
                 net.dn.push_back(D);
             }
-            if (nd < 2) return set_err(DF_ERR_UNSUPPORTED, "training needs conditioners of >= 2 Dense layers");
             t->lmax_h = std::max(t->lmax_h, nd - 1);
             t->any_pre = t->any_pre || net.pre;
             t->lnets.push_back(net);
@@ -592,7 +591,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
     auto fused_front = [&](const SweepOp& op) {
         const LNet& N = t->lnets[op.net];
         const int nd = (int)N.dn.size();
-        return keeps(op) && N.dn[nd - 1].fwd.mt <= 2 && N.dn[0].bwd.mt <= 4 && !no_fuse;
+        return nd >= 2 && keeps(op) && N.dn[nd - 1].fwd.mt <= 2 && N.dn[0].bwd.mt <= 4 && !no_fuse;
     };
     // H_k of a net: kept by the inverse pass, or recomputed into the shared buffers
     auto Hbuf = [&](const SweepOp& op, int k) -> float* {
@@ -688,6 +687,10 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             }
             if (k == 0) {
                 a.xsave = t->d_lx;
+                if (nd == 1) {  // a single-Dense conditioner: its input is the gathered features
+                    e = e == hipSuccess ? launch_gather_features(a, 16 * N.dn[0].bwd.mt, st) : e;
+                    a.in = t->d_lx;
+                }
             } else {
                 a.in = Hbuf(op, k - 1);
             }

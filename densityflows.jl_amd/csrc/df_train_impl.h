@@ -88,14 +88,29 @@ __device__ __forceinline__ void mul_act_grad(int act, const f32x4 (&y)[HT], f32x
     }
 }
 
-// accumulator-layout tile (rows 16m + 4g + r of sample j) → T[row][j]
+// Column-quad swizzle of the transpose buffers: quad q of row R is stored at quad
+// q ^ tswz((R >> 2) & 3), tswz = (0, 2, 3, 1).  A b128 read of (row j, quad g) then lands
+// on 16 distinct 4-bank groups in every 16-lane group of ds_read_b128.
+__device__ __forceinline__ int tswz(int q) { return DF_TRAIN_SWZ ? (0x78 >> (2 * (q & 3))) & 3 : 0; }
+// element (row, col) of a transpose buffer
+__device__ __forceinline__ int tidx(int row, int col) {
+    return row * kTS + ((((col >> 2) ^ tswz(row >> 2)) << 2) | (col & 3));
+}
+// f32x4 fragment (row, quad q) of a transpose buffer
+__device__ __forceinline__ f32x4 tread(const float* T, int row, int q) {
+    return *reinterpret_cast<const f32x4*>(T + row * kTS + ((q ^ tswz(row >> 2)) << 2));
+}
+
+// accumulator-layout tile (rows 16m + 4g + r of sample j) → T[row][j]; the row's
+// quad swizzle is tswz(g) for every (m, r), so the lane's column is loop-invariant
 template <int HT>
 __device__ __forceinline__ void t_write(float* T, const f32x4 (&v)[HT]) {
     const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+    const int col = (((j >> 2) ^ tswz(g)) << 2) | (j & 3);
 #pragma unroll
     for (int m = 0; m < HT; ++m)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) T[(16 * m + 4 * g + r) * kTS + j] = v[m][r];
+        for (int r = 0; r < 4; ++r) T[(16 * m + 4 * g + r) * kTS + col] = v[m][r];
 }
 
 __device__ __forceinline__ float hsum4(f32x4 v) { return (v[0] + v[1]) + (v[2] + v[3]); }
@@ -344,16 +359,16 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
         // ---- output Dense: dW3 += ȳ·hᵀ, db3 += Σȳ, h̄ = W3ᵀ ȳ ----
         if (g == 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) TA[r * kTS + j] = dout[r];
+            for (int r = 0; r < 4; ++r) TA[tidx(r, j)] = dout[r];
         }
         t_write<HT>(TB, H[0]);
         lds_order();
         {
-            const f32x4 fa = lds4f(TA + j * kTS + 4 * g);
+            const f32x4 fa = tread(TA, j, g);
             gbo += hsum4(fa);
 #pragma unroll
             for (int mb = 0; mb < HT; ++mb) {
-                const f32x4 fb = lds4f(TB + (16 * mb + j) * kTS + 4 * g);
+                const f32x4 fb = tread(TB, 16 * mb + j, g);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) gWo[mb] = mfma4(fa[q], fb[q], gWo[mb]);
             }
@@ -389,8 +404,8 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
             f32x4 fa[HT], fb[HT];
 #pragma unroll
             for (int m = 0; m < HT; ++m) {
-                fa[m] = lds4f(TA + (16 * m + j) * kTS + 4 * g);
-                fb[m] = lds4f(TB + (16 * m + j) * kTS + 4 * g);
+                fa[m] = tread(TA, 16 * m + j, g);
+                fb[m] = tread(TB, 16 * m + j, g);
                 gbh[m] += hsum4(fa[m]);
             }
             if constexpr (SPLIT) {
@@ -439,13 +454,13 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
         lds_order();
         t_write<HT>(TA, d0[0]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) TB[(4 * r + g) * kTS + j] = xin[0][r];
+        for (int r = 0; r < 4; ++r) TB[tidx(4 * r + g, j)] = xin[0][r];
         lds_order();
         {
-            const f32x4 fb = lds4f(TB + j * kTS + 4 * g);
+            const f32x4 fb = tread(TB, j, g);
 #pragma unroll
             for (int m = 0; m < HT; ++m) {
-                const f32x4 fa = lds4f(TA + (16 * m + j) * kTS + 4 * g);
+                const f32x4 fa = tread(TA, 16 * m + j, g);
                 gb0[m] += hsum4(fa);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) gW0[m] = mfma4(fa[q], fb[q], gW0[m]);

@@ -228,14 +228,13 @@ int df_random_normal(float* out, int64_t count, uint64_t seed, uint64_t offset, 
  * Adam state and the gradient buffer, and rewrites the chain's packed
  * weights after every update, so df_chain_* / df_flow_* calls on the chain
  * see the trained parameters.  Supported: every chain df_chain_create accepts
- * whose conditioners have >= 2 Denses (width <= 256, any depth, e.g. the
+ * (conditioner width <= 256, any depth — a single Dense included — e.g. the
  * hidden-256 config-5 model), with any of the nine DF_ACT_* activations; σ'
  * follows NNlib's derivative rules (from the output for relu / tanh_fast /
  * sigmoid_fast / leakyrelu / elu, from the pre-activation for softplus /
  * logcosh / swish).  Conditioners of the hidden <= 64, <= 4-output default
  * shape (_dflt_net, src/Layers.jl:33-50, n_sublayers <= 2) run one fused kernel
- * per net; the rest run the layer-wise MFMA path.  Single-Dense conditioners
- * return DF_ERR_UNSUPPORTED. */
+ * per net; the rest run the layer-wise MFMA path. */
 
 typedef struct df_train df_train;
 

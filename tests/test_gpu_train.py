@@ -16,7 +16,7 @@ import pytest
 
 import densityflows_amd as dfa
 from densityflows_amd.train import Adam, HIPTrainer, load_trainables, setup, train_, trainables
-from helpers import close, spec_to_element
+from helpers import _single_dense_spec, random_net, close, spec_to_element
 from oracle import flow_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -360,27 +360,25 @@ def test_train_matches_oracle_steps(cuda):
     assert np.mean(np.abs(got - p)) <= 1e-5
 
 
-def test_train_unsupported_structures(cuda):
-    """A conditioner of a single Dense has no hidden activation to train through
-    the kernels' Dense chain: refused, never silently handled elsewhere."""
+@pytest.mark.parametrize("B", [1000, 17])
+def test_gradient_parity_single_dense(cuda, B):
+    """Training through single-Dense conditioners (the layer-wise path: the features
+    gathered once, the output Dense + coupling pullback, x̄ = Wᵀȳ, dW = ȳ·xᵀ) against
+    the FD-pinned oracle gradient."""
     rng = np.random.default_rng(0)
-    ax = O.coupling_axes(4, [3, 4], n=0)
-    lay = dict(ax, kind="rnvp", s_net=_net(rng, [2, 2], ["identity"]), t_net=_net(rng, [2, 2], ["identity"]))
-    ch = spec_to_element({"kind": "chain", "layers": [lay]})
-    with pytest.raises(dfa.UnsupportedError):
-        HIPTrainer(ch.hip(), Adam())
-
-
-def _net(rng, dims, acts, bias_scale=0.1, out_scale=0.5):
-    """A Flux.Chain of Dense(dims[i], dims[i+1], acts[i]) (glorot W, U(±bias_scale) b)."""
-    net = []
-    for i in range(len(dims) - 1):
-        W = O.glorot_uniform(rng, dims[i + 1], dims[i])
-        if i == len(dims) - 2:
-            W = (W * np.float32(out_scale)).astype(np.float32)
-        b = ((rng.random(dims[i + 1]) * 2 - 1) * bias_scale).astype(np.float32)
-        net.append({"W": W, "b": b, "act": acts[i]})
-    return net
+    spec = _single_dense_spec(rng)
+    chain = spec_to_element(spec)
+    tr = HIPTrainer(chain.hip(), Adam())
+    np.testing.assert_array_equal(tr.get_params(), trainables(chain))
+    x, th = _inputs(5, 1, B)
+    g, lpsum = _gpu_grad(tr, x, th, cuda)
+    loss, ref = O.nll_and_grad(spec, x, th)
+    ref = _flat_oracle_grads(spec, ref)
+    assert g.shape == ref.shape
+    assert abs(-lpsum / B - loss) <= 1e-5 * max(1.0, abs(loss))
+    for sl in _tensor_slices(spec):
+        ok, r = close(g[sl], ref[sl], G_RTOL, G_ATOL)
+        assert ok, r
 
 
 OTHER_ACTS = ["softplus", "logcosh", "leakyrelu", "elu", "swish"]
@@ -424,8 +422,8 @@ def test_gradient_parity_docs_nets(cuda, out_act):
     Dense optionally carries an activation of its own."""
     rng = np.random.default_rng(6)
     ax = O.coupling_axes(8, [1, 3, 5, 7], n=1)
-    s_net = _net(rng, [5, 32, 16, 4], ["sigmoid", "relu", out_act])
-    t_net = _net(rng, [5, 12, 16, 32, 4], ["relu", "logcosh", "relu", out_act])
+    s_net = random_net(rng, [5, 32, 16, 4], ["sigmoid", "relu", out_act])
+    t_net = random_net(rng, [5, 12, 16, 32, 4], ["relu", "logcosh", "relu", out_act])
     spec = {"kind": "chain", "layers": [dict(ax, kind="rnvp", s_net=s_net, t_net=t_net),
                                         O.rnvp_layer(rng, O.reverse_axes(ax), hidden=16, act="swish",
                                                      bias_scale=0.1, out_scale=0.5)]}

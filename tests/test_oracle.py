@@ -240,6 +240,45 @@ def test_nll_gradient_other_activations_finite_differences(act):
     assert worst < 1e-5, worst
 
 
+def test_nll_gradient_single_dense_conditioners_finite_differences():
+    """Conditioners of one Dense (Chain(Dense(in, out, σ)), a legal s/t net in the
+    reference, src/affine/RNVP.jl:41-48): every weight and bias of the RNVP and NICE
+    single-Dense nets pinned by central finite differences."""
+    from helpers import _single_dense_spec
+
+    rng = np.random.default_rng(5)
+    chain = _single_dense_spec(rng)
+    x = rng.standard_normal((5, 9))
+    th = rng.random((1, 9))
+    _, grads = O.nll_and_grad(chain, x, th)
+
+    def loss_of():
+        z, l = O.backward(chain, x, th)
+        return -np.mean(O.mvnormal_logpdf(z) + l)
+
+    worst, checked = 0.0, 0
+    for li, L in enumerate(O._flat_layers(chain)):
+        for net in ("s_net", "t_net"):
+            if net not in L or len(L[net]) != 1:
+                continue
+            D = L[net][0]
+            for key in ("W", "b"):
+                D[key] = D[key].astype(np.float64)
+                for idx in np.ndindex(D[key].shape):
+                    orig = D[key][idx]
+                    h = 1e-6
+                    D[key][idx] = orig + h
+                    lp = loss_of()
+                    D[key][idx] = orig - h
+                    lm = loss_of()
+                    D[key][idx] = orig
+                    fd = (lp - lm) / (2 * h)
+                    g = grads[li][net][0][0 if key == "W" else 1][idx]
+                    worst = max(worst, abs(fd - g) / max(1e-6, abs(fd) + abs(g)))
+                    checked += 1
+    assert checked > 20 and worst < 1e-5, (checked, worst)
+
+
 def test_nll_gradient_sums_over_shards():
     """Per-shard gradients with the mean over the global batch sum to the full one."""
     rng = np.random.default_rng(1)
