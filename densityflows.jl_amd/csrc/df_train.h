@@ -30,14 +30,14 @@ namespace df {
 #endif
 constexpr int kTrainWaves = DF_TRAIN_WAVES;     // waves per workgroup of the fused net kernel
 constexpr int kTrainThreads = 64 * kTrainWaves;
-// Per-wave transpose buffers [row][16 samples] (df_train_impl.h).  DF_TRAIN_SWZ: rows of 16
-// floats with the 4-float column quads XOR-swizzled by row (trn::tswz), so the b128
-// fragment reads (row j, quad g) are bank-conflict free and the b32 row writes at most
-// 2-way (free for ds_write_b32); off: rows padded to 20 floats (reads 2-way).
+// Per-wave transpose buffers [row][16 samples] (df_train_impl.h): rows of 20 floats (row
+// R and R + 4 of a ds_write_b32 half-wave hit disjoint bank halves) and, with
+// DF_TRAIN_SWZ, the 4-float column quads XOR-swizzled by row (trn::tswz) so the b128
+// fragment reads (row j, quad g) are bank-conflict free too (off: 2-way).
 #ifndef DF_TRAIN_SWZ
 #define DF_TRAIN_SWZ 1
 #endif
-constexpr int kTS = DF_TRAIN_SWZ ? 16 : 20;  // row stride (floats)
+constexpr int kTS = 20;  // row stride (floats)
 
 namespace trn {
 // Activation modes of the training kernels: σ' from the output alone, relu-only,

@@ -89,9 +89,11 @@ __device__ __forceinline__ void mul_act_grad(int act, const f32x4 (&y)[HT], f32x
 }
 
 // Column-quad swizzle of the transpose buffers: quad q of row R is stored at quad
-// q ^ tswz((R >> 2) & 3), tswz = (0, 2, 3, 1).  A b128 read of (row j, quad g) then lands
-// on 16 distinct 4-bank groups in every 16-lane group of ds_read_b128.
-__device__ __forceinline__ int tswz(int q) { return DF_TRAIN_SWZ ? (0x78 >> (2 * (q & 3))) & 3 : 0; }
+// q ^ tswz(R >> 2), tswz(Q) = the Gray bit of Q & 3 (0, 1, 1, 0).  With the 20-float
+// rows, a b128 read of (row j, quad g) then lands on 16 distinct 4-bank groups in every
+// 16-lane group of ds_read_b128 (a search over all row swizzles); the b32
+// row writes keep their bank sets (a permutation inside the row).
+__device__ __forceinline__ int tswz(int q) { return DF_TRAIN_SWZ ? ((q ^ (q >> 1)) & 1) : 0; }
 // element (row, col) of a transpose buffer
 __device__ __forceinline__ int tidx(int row, int col) {
     return row * kTS + ((((col >> 2) ^ tswz(row >> 2)) << 2) | (col & 3));

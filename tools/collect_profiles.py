@@ -1,4 +1,4 @@
-"""Copy one measurement pass of tools/gpu_round2c.sh (gpurun_out/<tag>/) into profiles/<name>_*:
+"""Copy one measurement pass of tools/gpu_round3.sh (gpurun_out/<tag>/) into profiles/<name>_*:
 bench lines, rocprofv3 kernel-trace summaries and the PMC summaries of the forward and
 training kernels (tools/pmc_summary.py), each PMC file headed by the profiled source sha.
 
@@ -12,16 +12,22 @@ import sys
 tag, name, label = sys.argv[1], sys.argv[2], sys.argv[3]
 src = os.path.join("gpurun_out", tag)
 sha = open(os.path.join(src, "source_sha16.txt")).read().strip()
-for f in ("bench", "cfg1", "cfg1_4096", "cfg4", "nll", "train_cfg2", "train_cfg5"):
-    shutil.copy(os.path.join(src, f + ".json"), os.path.join("profiles", f"{name}_{f}.json"))
-for d, out in (("prof", "kernel_stats"), ("prof_cfg4", "cfg4_kernel_stats"),
+for f in ("bench_driver", "bench", "cfg1", "cfg1_4096", "cfg4", "nll", "train_cfg2", "train_cfg5"):
+    p = os.path.join(src, f + ".json")
+    if os.path.exists(p):
+        shutil.copy(p, os.path.join("profiles", f"{name}_{f}.json"))
+for d, out in (("prof_driver", "driver_cmd_kernel_stats"), ("prof", "kernel_stats"), ("prof_cfg4", "cfg4_kernel_stats"),
                ("prof_t2", "train_cfg2_kernel_stats"), ("prof_t5", "train_cfg5_kernel_stats")):
-    shutil.copy(os.path.join(src, d, "run_kernel_stats.csv"), os.path.join("profiles", f"{name}_{out}.csv"))
+    p = os.path.join(src, d, "run_kernel_stats.csv")
+    if os.path.exists(p):
+        shutil.copy(p, os.path.join("profiles", f"{name}_{out}.csv"))
 if os.path.exists(os.path.join(src, "pytest_gpu.log")):
     lines = open(os.path.join(src, "pytest_gpu.log")).read().splitlines()
-    keep = [l for l in lines if " PASSED" in l or " FAILED" in l or " ERROR" in l or "passed" in l]
+    keep = [l for l in lines if " PASSED" in l or " FAILED" in l or " ERROR" in l or " SKIPPED" in l or "passed" in l]
     with open(os.path.join("profiles", f"{name}_pytest_gpu_summary.txt"), "w") as fo:
         fo.write(f"# pytest -m gpu, {label}, source sha16 {sha}\n" + "\n".join(keep) + "\n")
+if os.path.exists(os.path.join(src, "smoke.log")):
+    shutil.copy(os.path.join(src, "smoke.log"), os.path.join("profiles", f"{name}_smoke.txt"))
 
 PMC = [
     ("pmc_cfg2", "cfg2 forward, FAST SPLIT kernel", [("uniform_kernel<4, 0", None)]),
@@ -35,8 +41,10 @@ PMC = [
 ]
 OUT = {"pmc_cfg2": "pmc_cfg2", "pmc_cfg4": "pmc_cfg4", "pmct_cfg2": "pmc_train_cfg2", "pmct_cfg4": "pmc_train_cfg5"}
 for d, what, kernels in PMC:
-    text = [f"# rocprofv3 PMC passes (tools/pmc_sets.txt, one counter set per run), {what}, {label} (tools/gpu_round2c.sh)",
-            f"# source sha16 {sha}"]
+    if not os.path.isdir(os.path.join(src, d)):
+        continue
+    text = [f"# rocprofv3 PMC passes (tools/pmc_sets.txt, one counter set per run), {what}, {label} "
+            f"(tools/gpu_round3.sh)", f"# source sha16 {sha}"]
     for sub, head in kernels:
         r = subprocess.run([sys.executable, "tools/pmc_summary.py", f"{tag}/{d}", sub],
                            capture_output=True, text=True, check=True)

@@ -1,19 +1,23 @@
 #!/bin/bash
-# GPU box, round-2 final measurement pass: full -m gpu suite, smoke, headline bench
-# (+ exact-f32 side timing), kernel traces, secondary benches, PMC of the headline and
-# config-4 forward kernels and of the config-2 / config-5 train steps (one counter set per run).
+# GPU box, round-3 measurement pass: the -m gpu suite, smoke, the driver's bench command
+# (and a longer run), every secondary workload, kernel traces (the driver's exact command
+# included) and PMC passes (tools/pmc_sets.txt, one counter set per run) of the forward
+# and training kernels.  Collected into profiles/ by tools/collect_profiles.py.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/${1:-r2c}
+O=gpurun_out/${1:-r3}
 mkdir -p $O
 python3 -c "import bench; print(bench.source_sha16())" > $O/source_sha16.txt
-timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf -s --timeout 180 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rs --timeout 180 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc $rc" >> $O/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
-timeout -k 10 240 python bench.py --cpu-seconds 15 > $O/bench.json 2> $O/bench.err && \
+timeout -k 10 240 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err && \
+timeout -k 10 240 python3 bench.py --steps 200 --warmup 50 --cpu-seconds 15 > $O/bench.json 2> $O/bench.err && \
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_driver -o run -- \
+    python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/prof_driver.log 2>&1 && \
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
     python3 bench.py --no-cpu > $O/prof.log 2>&1 && \
 timeout -k 10 240 python bench.py --config cfg1 --batch 4096 --steps 500 --warmup 100 --cpu-seconds 10 > $O/cfg1_4096.json 2> $O/cfg1_4096.err && \
@@ -36,7 +40,7 @@ for cfg in cfg2 cfg4; do
     [ -z "$line" ] && continue
     i=$((i+1))
     timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $line --output-format csv -d $O/pmc_${cfg}/p$i -o run -- \
-        python3 bench.py --config $cfg --steps $steps --warmup 1 --no-cpu --no-exact > $O/pmc_${cfg}_p$i.log 2>&1 || exit 1
+        python3 bench.py --config $cfg --steps $steps --warmup 1 --no-cpu --no-exact --settle-seconds 0 > $O/pmc_${cfg}_p$i.log 2>&1 || exit 1
   done < tools/pmc_sets.txt
 done
 for cfg in cfg2 cfg4; do
@@ -45,6 +49,6 @@ for cfg in cfg2 cfg4; do
     [ -z "$line" ] && continue
     i=$((i+1))
     timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $line --output-format csv -d $O/pmct_${cfg}/p$i -o run -- \
-        python3 bench.py --mode train --config $cfg --steps $steps --warmup 1 --no-cpu > $O/pmct_${cfg}_p$i.log 2>&1 || exit 1
+        python3 bench.py --mode train --config $cfg --steps $steps --warmup 1 --no-cpu --settle-seconds 0 > $O/pmct_${cfg}_p$i.log 2>&1 || exit 1
   done < tools/pmc_sets.txt
 done

@@ -37,6 +37,11 @@ if dur:
                   "SQ_ACTIVE_INST_LDS", "SQ_WAIT_INST_LDS"):
             if k in tot:
                 print(f"{k} / SQ_WAVE_CYCLES {tot[k] / tot['SQ_WAVE_CYCLES']:.3f}")
+    if "SQ_VALU_MFMA_COEXEC_CYCLES" in tot and "SQ_VALU_MFMA_BUSY_CYCLES" in tot:
+        print(f"VALU co-executing with MFMA / MFMA busy cycles "
+              f"{tot['SQ_VALU_MFMA_COEXEC_CYCLES'] / tot['SQ_VALU_MFMA_BUSY_CYCLES']:.3f}")
+    if "SQ_LDS_BANK_CONFLICT" in tot and tot.get("SQ_INSTS_LDS"):
+        print(f"LDS bank-conflict cycles per LDS instruction {tot['SQ_LDS_BANK_CONFLICT'] / tot['SQ_INSTS_LDS']:.3f}")
     if "FETCH_SIZE" in tot and "WRITE_SIZE" in tot:
         b = (2.0 * tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024.0
         print(f"HBM traffic per dispatch {b/1e6:.2f} MB ((2*FETCH_SIZE + WRITE_SIZE) KiB)")
