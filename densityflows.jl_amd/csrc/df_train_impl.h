@@ -139,11 +139,24 @@ __device__ __forceinline__ uni::bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// dW_out and dW0 of the SPLIT instances (one first-Dense k-step: <= 4 features, <= 4
+// outputs) on v_mfma_f32_4x4x1_16b_f32: 16 blocks of 4×4, one sample per instruction,
+// block b = lane / 4 owning hidden rows 4b..4b+3 — no zero-padded rows (the 16x16x4
+// form spends 12 of its 16 rows on padding there).  Lane l then holds dW_out[0..3][l]
+// and dW0[4(l/4) + 0..3][l % 4].
+#ifndef DF_TRAIN_M4
+#define DF_TRAIN_M4 1
+#endif
+__device__ __forceinline__ f32x4 mfma4x4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
+
 template <int HT, int NH, int AM, bool SPLIT = false>
 __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a) {
     using namespace trn;
     constexpr bool RELU = (AM == AM_RELU);
     constexpr bool PRE = (AM == AM_PRE);
+    constexpr bool M4 = SPLIT && DF_TRAIN_M4;
     static_assert(!SPLIT || (RELU && NH == 1 && HT >= 2), "SPLIT: relu nets with one hidden Dense, hidden 32/64");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const GNet& G = a.net;
@@ -182,6 +195,9 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
     constexpr int NHT = NH ? HT : 1;
     f32x4 gW0[HT], gWo[HT], gWh[NHT][NHT];
     float gb0[HT], gbh[NHT], gbo = 0.f;
+    f32x4 gWo4 = f32x4{0.f, 0.f, 0.f, 0.f}, gW04 = f32x4{0.f, 0.f, 0.f, 0.f};  // M4 accumulators
+    float gb0l = 0.f;                                                          // M4: Σ δ0[lane]
+    const int lrow = lane < TROWS ? lane : TROWS - 1;  // M4 operand row of this lane (clamped)
 #pragma unroll
     for (int m = 0; m < HT; ++m) {
         gW0[m] = gWo[m] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -365,7 +381,20 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
         }
         t_write<HT>(TB, H[0]);
         lds_order();
-        {
+        if constexpr (M4) {  // block b: A = ȳ[lane % 4][s], B = h[lane][s], one sample s per step
+            const f32x4 fa = tread(TA, j, g);
+            gbo += hsum4(fa);
+            f32x4 yv[4], hv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                yv[q] = tread(TA, lane & 3, q);
+                hv[q] = tread(TB, lrow, q);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) gWo4 = mfma4x4(yv[q][e], hv[q][e], gWo4);
+        } else {
             const f32x4 fa = tread(TA, j, g);
             gbo += hsum4(fa);
 #pragma unroll
@@ -458,7 +487,19 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
 #pragma unroll
         for (int r = 0; r < 4; ++r) TB[tidx(4 * r + g, j)] = xin[0][r];
         lds_order();
-        {
+        if constexpr (M4) {  // block b: A = δ0[lane][s], B = x[lane % 4][s]
+            f32x4 dv[4], xv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                dv[q] = tread(TA, lrow, q);
+                xv[q] = tread(TB, lane & 3, q);
+            }
+            gb0l += (hsum4(dv[0]) + hsum4(dv[1])) + (hsum4(dv[2]) + hsum4(dv[3]));
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) gW04 = mfma4x4(dv[q][e], xv[q][e], gW04);
+        } else {
             const f32x4 fb = tread(TB, j, g);
 #pragma unroll
             for (int m = 0; m < HT; ++m) {
@@ -504,20 +545,31 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
     const int wo2 = G.w_off[2] - G.p_begin, bo2 = G.b_off[2] - G.p_begin;
     for (int w = 0; w < kTrainWaves; ++w) {
         if (wave == w) {
+            if constexpr (M4) {
 #pragma unroll
-            for (int m = 0; m < HT; ++m)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = 16 * m + 4 * g + r;
-                    if (row < h && j < G.n_in) R[wo0 + row + h * j] += gW0[m][r];
-                    const int ob = 16 * m + j;  // output Dense: row o = 4g + r, column ob
-                    if (4 * g + r < N.n_out && ob < h) R[wo2 + (4 * g + r) + N.n_out * ob] += gWo[m][r];
+                for (int i = 0; i < 4; ++i) {
+                    if (i < N.n_out && lane < h) R[wo2 + i + N.n_out * lane] += gWo4[i];
+                    const int row = 4 * (lane >> 2) + i, col = lane & 3;
+                    if (row < h && col < G.n_in) R[wo0 + row + h * col] += gW04[i];
                 }
-            if (g == 0) {
+                if (G.b_off[0] >= 0 && lane < h) R[bo0 + lane] += gb0l;
+                if (g == 0 && G.b_off[2] >= 0 && j < N.n_out) R[bo2 + j] += gbo;
+            } else {
 #pragma unroll
                 for (int m = 0; m < HT; ++m)
-                    if (G.b_off[0] >= 0 && 16 * m + j < h) R[bo0 + 16 * m + j] += gb0[m];
-                if (G.b_off[2] >= 0 && j < N.n_out) R[bo2 + j] += gbo;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = 16 * m + 4 * g + r;
+                        if (row < h && j < G.n_in) R[wo0 + row + h * j] += gW0[m][r];
+                        const int ob = 16 * m + j;  // output Dense: row o = 4g + r, column ob
+                        if (4 * g + r < N.n_out && ob < h) R[wo2 + (4 * g + r) + N.n_out * ob] += gWo[m][r];
+                    }
+                if (g == 0) {
+#pragma unroll
+                    for (int m = 0; m < HT; ++m)
+                        if (G.b_off[0] >= 0 && 16 * m + j < h) R[bo0 + 16 * m + j] += gb0[m];
+                    if (G.b_off[2] >= 0 && j < N.n_out) R[bo2 + j] += gbo;
+                }
             }
             if constexpr (NH == 1) {
 #pragma unroll
