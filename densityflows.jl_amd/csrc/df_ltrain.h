@@ -33,7 +33,15 @@ constexpr int kLChunkBytes = 32 * 1024;  // weight chunk (LDS, double-buffered)
 #endif
 constexpr int kLTiles = DF_LTILES;       // 16-sample tiles per wave per round
 constexpr size_t kLdwLdsMax = 80 * 1024; // dW staging LDS (32 or 64 samples per step)
-constexpr size_t kLdwSplitLds = 2 * 3 * 256 * 80;  // SPLIT dW: both operands' planes, [p][row][32 samples + pad]
+#ifndef DF_LDW_DMA
+#define DF_LDW_DMA 1
+#endif
+#if DF_LDW_DMA  // SPLIT dW: f32 stage of both operands (32 sample rows) + their bf16x3 planes
+constexpr size_t kLdwSplitLds = 2 * 32 * 256 * 4 + 2 * 3 * 256 * 64;
+#else           // SPLIT dW: both operands' planes, [p][row][32 samples + pad]
+constexpr size_t kLdwSplitLds = 2 * 3 * 256 * 80;
+#endif
+constexpr int kLdwSplitThreads = 256;              // SPLIT dW kernel: one wave per SIMD
 constexpr int kLdwBM = 8;                // per-wave output blocks (16×16): up to 8 row tiles
 constexpr int kLdwBN = 4;                //   × 4 column tiles (128 accumulator registers)
 
@@ -89,10 +97,10 @@ struct LdwArgs {
     int64_t p_total;
     int w_off, b_off;       // trainables offsets (b_off -1: no bias)
     int64_t batch;
-    int split;              // 1: bf16x3 split products (ldw_split_body; mta = ntb = 16)
+    int split;              // 1: bf16x3 split products (ldw_split_kernel, its own launch; mta = ntb = 16)
 };
 
-// One merged launch: up to three dW products (ldw) of net i and, optionally, the
+// One merged launch: up to three non-split dW products (ldw) of net i and, optionally, the
 // couple_bwd front of net i+1 (sweep_kernel, df_ltrain.hip).
 struct SweepJob {
     LdwArgs w[3];

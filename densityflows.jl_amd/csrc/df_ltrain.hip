@@ -611,64 +611,218 @@ __device__ __forceinline__ void ldw_body(const LdwArgs& a, float* lsm, int bid, 
     }
 }
 
-// dW = δ·inᵀ of a 256×256 Dense on bf16x3 split products (LdwArgs::split): each
-// staging step of 32 samples writes both operands to LDS as planes [p][row][sample]
-// (80-byte rows: the 16 rows × 4 lane groups of a ds_read_b128 hit 64 distinct banks),
-// split once per element; a wave's 8 × 4 blocks of 16×16 then take six bf16 MFMAs per
-// block and step (k = 32 samples).  A thread stages (row, 8 samples) items of both
-// operands (8 strided dword loads per item, lanes on consecutive rows: coalesced),
-// loaded one step ahead, and keeps the f32 sum of its δ items for db.
-__device__ __forceinline__ void ldw_split_body(const LdwArgs& a, uint8_t* lsm, int bid, int nblk) {
-    constexpr int RS = 80;                       // bytes per staged row (32 bf16 + pad)
-    constexpr int PB = 256 * RS;                 // bytes per plane
-    uint8_t* TA = lsm;                           // δ planes
-    uint8_t* TB = lsm + 3 * PB;                  // in planes
-    float* dbr = reinterpret_cast<float*>(lsm);  // db reduction (after the last step)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// The 256×256 split dW on one wave per SIMD: 4 waves in a 2 × 2 grid of 128 × 128
+// quadrants, each wave 8 × 8 blocks of 16×16 (256 accumulator registers: the AGPR half
+// of the 512-entry file a lone wave owns).
+//
+// DF_LDW_DMA (default): per 32-sample step,
+//   1. the f32 rows of both operands arrive HBM → LDS by the DMA path (global_load_lds,
+//      16 B a lane: one sample row of 256 floats per instruction), issued a whole step
+//      ahead (under the previous step's MFMAs) with no registers held for them;
+//   2. the workgroup splits every element once: thread (row quad q, sample group sg) of
+//      each operand reads its 4 rows × 8 samples (8 ds_read_b128), splits each row's
+//      8 samples into three bf16 planes and writes them to LDS as [p][row][32 samples]
+//      (64-byte rows; sample-group slot sg ^ ((−row >> 2) & 3), so the fragment
+//      ds_read_b128 of the MFMA phase hit 64 distinct banks; the writes are 2-way);
+//   3. each wave runs 6 MFMAs per block from the planes (48 ds_read_b128 per 384 MFMAs).
+// LDS: 64 KiB f32 stage + 96 KiB planes = the whole 160 KiB; two barriers per step.
+// Otherwise: the round-3 form (register prefetch, planes with 80-byte rows).
+// db: the f32 sums of each δ row's four 8-sample groups, summed in group order; both
+// forms give bitwise the same partial rows for the same grid.
+// DF_LDW_DIAG (timing diagnostics, wrong results): 1 = no MFMA phase, 2 = no split phase
+#ifndef DF_LDW_DIAG
+#define DF_LDW_DIAG 0
+#endif
+#if DF_LDW_DMA
+__device__ __forceinline__ int ldw_slot(int row, int sg) { return sg ^ ((-(row >> 2)) & 3); }
+
+__global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lsm_f[];
+    constexpr int PB = 256 * 64;  // bytes per plane
+    float* stage = lsm_f;         // [op][32 samples][256]
+    uint8_t* TA = reinterpret_cast<uint8_t*>(lsm_f + 2 * 32 * 256);  // δ planes [p][row][64 B]
+    uint8_t* TB = TA + 3 * PB;                                       // in planes
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, j = lane & 15;
-    const int wi = wave % a.wm, wj = wave / a.wm;
-    const int m0 = wi * a.bm, n0 = wj * a.bn;
+    const int m0 = 8 * (wave & 1), n0 = 8 * (wave >> 1);
+    const int q = lane, sg = wave;  // this thread's staging item of each operand: rows 4q.., samples 8sg..
+    const int nblk = gridDim.x;
     const int64_t per = (a.batch + nblk - 1) / nblk;
-    const int64_t s_begin = (int64_t)bid * per;
+    const int64_t s_begin = (int64_t)blockIdx.x * per;
     const int64_t s_end = (s_begin + per < a.batch) ? s_begin + per : a.batch;
 
-    f32x4 acc[kLdwBM][kLdwBN];
+    f32x4 acc[8][8];
 #pragma unroll
-    for (int im = 0; im < kLdwBM; ++im)
+    for (int im = 0; im < 8; ++im)
 #pragma unroll
-        for (int in = 0; in < kLdwBN; ++in) acc[im][in] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int in = 0; in < 8; ++in) acc[im][in] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dbp[4] = {0.f, 0.f, 0.f, 0.f};  // rows 4q + i, sample group sg
 
-    // staging items: q = tid + k·512, k < 2 → operand A (1024 items: row q & 255, samples 8(q >> 8)..),
-    // k >= 2 → operand B; 4 items per thread, each 8 samples of one row
-    float pv[4][8];
-    float dbp[2] = {0.f, 0.f};
-    auto fetch = [&](int64_t s0) {
+    // sample rows s = wave, wave + 4, .. of both operands (64 per step); a sample past
+    // the workgroup's range is a row of zeros instead
+    auto dma = [&](int64_t s0) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int q = (tid + (k & 1) * kBlockThreads);
-            const int row = q & 255, sg = q >> 8;
-            const float* src = (k < 2) ? a.da : a.xb;
-            const int ld = (k < 2) ? a.lda : a.ldb;
-            const int rmax = (k < 2) ? a.m_true : a.n_true;
+        for (int k = 0; k < 16; ++k) {
+            const int r = wave + 4 * k, op = r >> 5, s = r & 31;
+            float* dst = stage + (op * 32 + s) * 256;
+            if (s0 + s < s_end) {
+                const float* src = (op ? a.xb + (s0 + s) * a.ldb : a.da + (s0 + s) * a.lda) + 4 * lane;
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                                 (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+            } else {
+                *reinterpret_cast<f32x4*>(dst + 4 * lane) = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    };
+    // step 2 for one operand: rows 4q + i, samples 8sg + e
+    auto split_item = [&](int op, uint8_t* T, bool db) {
+        f32x4 x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = *reinterpret_cast<const f32x4*>(stage + (op * 32 + 8 * sg + e) * 256 + 4 * q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float v[8] = {x[0][i], x[1][i], x[2][i], x[3][i], x[4][i], x[5][i], x[6][i], x[7][i]};
+            uni::bf16x8 p0, p1, p2;
+            uni::split8(v, p0, p1, p2);
+            const int row = 4 * q + i;
+            uint8_t* dst = T + row * 64 + 16 * ldw_slot(row, sg);
+            *reinterpret_cast<uni::bf16x8*>(dst) = p0;
+            *reinterpret_cast<uni::bf16x8*>(dst + PB) = p1;
+            *reinterpret_cast<uni::bf16x8*>(dst + 2 * PB) = p2;
+            if (db) {
+                float sum = dbp[i];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sum = sum + v[e];
+                dbp[i] = sum;
+            }
+        }
+    };
+    auto frag = [&](const uint8_t* T, int row, uni::bf16x8 (&p)[3]) {
+        const uint8_t* src = T + row * 64 + 16 * ldw_slot(row, g);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) p[k] = *reinterpret_cast<const uni::bf16x8*>(src + k * PB);
+    };
+
+    if (s_begin < s_end) dma(s_begin);
+    for (int64_t s0 = s_begin; s0 < s_end; s0 += 32) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's rows of the step landed
+        __syncthreads();                                     // ... every wave's; the planes are free
+#if DF_LDW_DIAG != 2
+        split_item(0, TA, true);
+        split_item(1, TB, false);
+#endif
+        __syncthreads();                                     // planes written; the stage is free
+        if (s0 + 32 < s_end) dma(s0 + 32);
+#if DF_LDW_DIAG == 1
+        continue;
+#endif
+        uni::bf16x8 xb[8][3];
+#pragma unroll
+        for (int in = 0; in < 8; ++in) frag(TB, 16 * (n0 + in) + j, xb[in]);
+#pragma unroll
+        for (int im = 0; im < 8; ++im) {
+            uni::bf16x8 wa[3];
+            frag(TA, 16 * (m0 + im) + j, wa);
+#pragma unroll
+            for (int in = 0; in < 8; ++in) {  // small terms first
+                f32x4 v4 = acc[im][in];
+                v4 = uni::mfma_bf(wa[2], xb[in][0], v4);
+                v4 = uni::mfma_bf(wa[1], xb[in][1], v4);
+                v4 = uni::mfma_bf(wa[0], xb[in][2], v4);
+                v4 = uni::mfma_bf(wa[1], xb[in][0], v4);
+                v4 = uni::mfma_bf(wa[0], xb[in][1], v4);
+                acc[im][in] = uni::mfma_bf(wa[0], xb[in][0], v4);
+            }
+        }
+    }
+
+    float* dst = a.partial + (int64_t)blockIdx.x * a.p_total;
+#pragma unroll
+    for (int im = 0; im < 8; ++im)
+#pragma unroll
+        for (int in = 0; in < 8; ++in)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * (m0 + im) + 4 * g + r, col = 16 * (n0 + in) + j;
+                if (row < a.m_true && col < a.n_true) dst[a.w_off + row + (int64_t)a.m_true * col] = acc[im][in][r];
+            }
+    // db[row] = Σ of the row's four sample groups, in group order
+    __syncthreads();
+    float* dbl = lsm_f;  // [group][row]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dbl[256 * sg + 4 * q + i] = dbp[i];
+    __syncthreads();
+    if (a.b_off >= 0 && tid < a.m_true)
+        dst[a.b_off + tid] = ((dbl[tid] + dbl[256 + tid]) + dbl[512 + tid]) + dbl[768 + tid];
+}
+#else
+// Round-3 form: each staging step of 32 samples writes both operands to LDS as planes
+// [p][row][sample] (80-byte rows: the 16 rows × 4 lane groups of a ds_read_b128 hit 64
+// distinct banks), split once per element; a thread stages row tid of both operands
+// (8 strided dword loads per 8 samples, lanes on consecutive rows: coalesced), loaded
+// one step ahead, and keeps the f32 sums of its δ row's four sample groups for db.
+__global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lsm_f[];
+    uint8_t* lsm = reinterpret_cast<uint8_t*>(lsm_f);
+    constexpr int RS = 80;
+    constexpr int PB = 256 * RS;
+    constexpr int NT = kLdwSplitThreads;
+    uint8_t* TA = lsm;
+    uint8_t* TB = lsm + 3 * PB;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, j = lane & 15;
+    const int m0 = 8 * (wave & 1), n0 = 8 * (wave >> 1);
+    const int nblk = gridDim.x;
+    const int64_t per = (a.batch + nblk - 1) / nblk;
+    const int64_t s_begin = (int64_t)blockIdx.x * per;
+    const int64_t s_end = (s_begin + per < a.batch) ? s_begin + per : a.batch;
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int im = 0; im < 8; ++im)
+#pragma unroll
+        for (int in = 0; in < 8; ++in) acc[im][in] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // items q = tid + 256k: k < 4 → operand A (row tid, samples 8k..8k+7), k >= 4 → operand B
+    float pv[8][8];
+    float dbp[4] = {0.f, 0.f, 0.f, 0.f};
+    // a whole step of full rows (uniform test): unguarded loads, which the compiler keeps
+    // in one basic block; the batch tail and narrower rows take the guarded copy
+    const bool full_rows = a.m_true == 256 && a.n_true == 256;
+    auto fetch = [&](int64_t s0) {
+        if (full_rows && s0 + 32 <= s_end) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float* src = ((k < 4) ? a.da : a.xb) + (s0 + 8 * (k & 3)) * ((k < 4) ? a.lda : a.ldb) + tid;
+                const int ld = (k < 4) ? a.lda : a.ldb;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) pv[k][e] = src[e * ld];
+            }
+            return;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int sg = k & 3;
+            const float* src = (k < 4) ? a.da : a.xb;
+            const int ld = (k < 4) ? a.lda : a.ldb;
+            const int rmax = (k < 4) ? a.m_true : a.n_true;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const int64_t smp = s0 + 8 * sg + e;
-                pv[k][e] = (smp < s_end && row < rmax) ? src[smp * ld + row] : 0.f;
+                pv[k][e] = (smp < s_end && tid < rmax) ? src[smp * ld + tid] : 0.f;
             }
         }
     };
     auto stash = [&]() {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int q = (tid + (k & 1) * kBlockThreads);
-            const int row = q & 255, sg = q >> 8;
+        for (int k = 0; k < 8; ++k) {
             uni::bf16x8 x0, x1, x2;
             uni::split8(pv[k], x0, x1, x2);
-            uint8_t* base = ((k < 2) ? TA : TB) + row * RS + 16 * sg;
+            uint8_t* base = ((k < 4) ? TA : TB) + tid * RS + 16 * (k & 3);
             *reinterpret_cast<uni::bf16x8*>(base) = x0;
             *reinterpret_cast<uni::bf16x8*>(base + PB) = x1;
             *reinterpret_cast<uni::bf16x8*>(base + 2 * PB) = x2;
-            if (k < 2) {  // db: this thread's 8 samples of row q & 255, in sample order
+            if (k < 4) {
                 float sum = dbp[k];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) sum = sum + pv[k][e];
@@ -679,25 +833,24 @@ __device__ __forceinline__ void ldw_split_body(const LdwArgs& a, uint8_t* lsm, i
 
     if (s_begin < s_end) fetch(s_begin);
     for (int64_t s0 = s_begin; s0 < s_end; s0 += 32) {
-        __syncthreads();  // previous step consumed
+        __syncthreads();
         stash();
         __syncthreads();
         if (s0 + 32 < s_end) fetch(s0 + 32);
-        // B planes of this wave's column blocks (rows 16(n0 + in) + j, samples 8g..8g+7)
-        uni::bf16x8 xb[kLdwBN][3];
+        uni::bf16x8 xb[8][3];
 #pragma unroll
-        for (int in = 0; in < kLdwBN; ++in)
+        for (int in = 0; in < 8; ++in)
 #pragma unroll
             for (int p = 0; p < 3; ++p)
                 xb[in][p] = *reinterpret_cast<const uni::bf16x8*>(TB + p * PB + (16 * (n0 + in) + j) * RS + 16 * g);
 #pragma unroll
-        for (int im = 0; im < kLdwBM; ++im) {
+        for (int im = 0; im < 8; ++im) {
             uni::bf16x8 wa[3];
 #pragma unroll
             for (int p = 0; p < 3; ++p)
                 wa[p] = *reinterpret_cast<const uni::bf16x8*>(TA + p * PB + (16 * (m0 + im) + j) * RS + 16 * g);
 #pragma unroll
-            for (int in = 0; in < kLdwBN; ++in) {  // small terms first
+            for (int in = 0; in < 8; ++in) {  // small terms first
                 f32x4 v = acc[im][in];
                 v = uni::mfma_bf(wa[2], xb[in][0], v);
                 v = uni::mfma_bf(wa[1], xb[in][1], v);
@@ -709,44 +862,34 @@ __device__ __forceinline__ void ldw_split_body(const LdwArgs& a, uint8_t* lsm, i
         }
     }
 
-    float* dst = a.partial + (int64_t)bid * a.p_total;
+    float* dst = a.partial + (int64_t)blockIdx.x * a.p_total;
 #pragma unroll
-    for (int im = 0; im < kLdwBM; ++im) {
-        const int ma = m0 + im;
+    for (int im = 0; im < 8; ++im)
 #pragma unroll
-        for (int in = 0; in < kLdwBN; ++in) {
-            const int nbk = n0 + in;
+        for (int in = 0; in < 8; ++in)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = 16 * ma + 4 * g + r, col = 16 * nbk + j;
+                const int row = 16 * (m0 + im) + 4 * g + r, col = 16 * (n0 + in) + j;
                 if (row < a.m_true && col < a.n_true) dst[a.w_off + row + (int64_t)a.m_true * col] = acc[im][in][r];
             }
-        }
-    }
-    // db[row] = Σ over the workgroup's samples: the four sample groups of a row in order
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 2; ++k) dbr[tid + k * kBlockThreads] = dbp[k];
-    __syncthreads();
-    if (a.b_off >= 0 && tid < a.m_true) {
-        const float v = ((dbr[tid] + dbr[tid + 256]) + dbr[tid + 512]) + dbr[tid + 768];
-        dst[a.b_off + tid] = v;
-    }
+    // db[row] = Σ of the row's four sample groups, in group order
+    if (a.b_off >= 0 && tid < a.m_true) dst[a.b_off + tid] = ((dbp[0] + dbp[1]) + dbp[2]) + dbp[3];
 }
+
+#endif  // DF_LDW_DMA
 
 template <int S, int BMX, int BNX>
 __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lsm[];
-    if (a.split) ldw_split_body(a, reinterpret_cast<uint8_t*>(lsm), blockIdx.x, gridDim.x);
-    else ldw_body<S, BMX, BNX>(a, lsm, blockIdx.x, gridDim.x);
+    ldw_body<S, BMX, BNX>(a, lsm, blockIdx.x, gridDim.x);
 }
 
-// One merged launch of the sweep: the dW products of net i (each workgroup's
+// One merged launch of the sweep: the non-split dW products of net i (each workgroup's
 // split-K share, as ldw_kernel) and the output-Dense/pullback front of net i+1
 // (couple_body, which depends only on z̄ after net i's W1ᵀδ1 kernel).  Even
-// workgroups run the front first, odd ones the dW products first, so the
-// HBM-bound front of one half of the CUs runs beside the MFMA-bound dW1 of the other
-// half instead of after it (and the two narrow, HBM-bound dW products likewise).
+// workgroups run the front first, odd ones the dW products first, so the fronts and the
+// narrow products of the two halves of the CUs interleave.  (The split 256×256 dW is
+// its own launch, ldw_split_kernel: one wave per SIMD.)
 template <int HT, int MTO>
 __global__ void __launch_bounds__(kBlockThreads, 1) sweep_kernel(SweepJob j) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -758,9 +901,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) sweep_kernel(SweepJob j) {
         }
     }
     for (int k = 0; k < j.nw; ++k) {
-        if (j.w[k].split)
-            ldw_split_body(j.w[k], smem, blockIdx.x, gridDim.x);
-        else if (j.ws[k] == 64)
+        if (j.ws[k] == 64)
             ldw_body<64, 2, 2>(j.w[k], reinterpret_cast<float*>(smem), blockIdx.x, gridDim.x);
         else
             ldw_body<32, kLdwBM, kLdwBN>(j.w[k], reinterpret_cast<float*>(smem), blockIdx.x, gridDim.x);
@@ -860,6 +1001,9 @@ hipError_t set_ldense_lds_limit(size_t lds) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_kernel<32, kLdwBM, kLdwBN>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldw_lds_bytes());
     if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_split_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kLdwSplitLds);
+    if (e != hipSuccess) return e;
     return hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_kernel<64, 2, 2>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)ldw_lds_bytes());
 }
@@ -894,7 +1038,7 @@ static size_t ldw_stage_bytes(int S, int mta, int ntb) { return (size_t)S * (16 
 static int ldw_samples(const LdwArgs& a) {
     return (a.bm <= 2 && a.bn <= 2 && ldw_stage_bytes(64, a.mta, a.ntb) <= kLdwLdsMax) ? 64 : 32;
 }
-size_t ldw_lds_bytes() { return kLdwSplitLds > kLdwLdsMax ? kLdwSplitLds : kLdwLdsMax; }
+size_t ldw_lds_bytes() { return kLdwLdsMax; }
 
 bool ldw_shape(int mta, int ntb, int* wm, int* bm, int* bn) {
     int best = 1 << 30;
@@ -937,11 +1081,15 @@ hipError_t launch_sweep(int ht, int mto, const SweepJob& j, unsigned grid, size_
 
 hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st) {
     void* args[] = {const_cast<LdwArgs*>(&a)};
+    if (a.split) {
+        if (a.mta != 16 || a.ntb != 16) return hipErrorInvalidValue;  // the kernel's fixed 256×256 shape
+        return hipLaunchKernel(reinterpret_cast<void*>(&ldw_split_kernel), dim3(grid), dim3(kLdwSplitThreads), args,
+                               kLdwSplitLds, st);
+    }
     const int S = ldw_samples(a);
     void* fn = S == 64 ? reinterpret_cast<void*>(&ldw_kernel<64, 2, 2>)
                        : reinterpret_cast<void*>(&ldw_kernel<32, kLdwBM, kLdwBN>);
-    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args,
-                           a.split ? kLdwSplitLds : ldw_stage_bytes(S, a.mta, a.ntb), st);
+    return hipLaunchKernel(fn, dim3(grid), dim3(kBlockThreads), args, ldw_stage_bytes(S, a.mta, a.ntb), st);
 }
 
 }  // namespace df

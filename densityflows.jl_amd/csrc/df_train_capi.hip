@@ -768,6 +768,16 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         int rc = dw_args(op, par, jobs);
         if (rc != DF_OK) return rc;
         front_done = false;
+        // the split 256×256 dW runs as its own launch (one wave per SIMD, ldw_split_kernel)
+        for (auto it = jobs.begin(); it != jobs.end();) {
+            if (!it->split) {
+                ++it;
+                continue;
+            }
+            e = launch_ldw(*it, (unsigned)t->lgrid, st);
+            if (e != hipSuccess) return hip_err(e, "split dW kernel launch");
+            it = jobs.erase(it);
+        }
         if (!no_merge && jobs.size() <= 3) {
             SweepJob j{};
             // narrow (HBM-bound) products first, the hidden×hidden one last: even
