@@ -32,8 +32,8 @@ constexpr int kTrainWaves = DF_TRAIN_WAVES;     // waves per workgroup of the fu
 constexpr int kTrainThreads = 64 * kTrainWaves;
 // Per-wave transpose buffers [row][16 samples] (df_train_impl.h): rows of 20 floats (row
 // R and R + 4 of a ds_write_b32 half-wave hit disjoint bank halves) and, with
-// DF_TRAIN_SWZ, the 4-float column quads XOR-swizzled by row (trn::tswz) so the b128
-// fragment reads (row j, quad g) are bank-conflict free too (off: 2-way).
+// DF_TRAIN_SWZ, the 4-float column quads XOR-swizzled by row (trn::rswz: Gray bit of
+// (R >> 2) & 3 ^ bit 4 of R) so both b128 fragment read shapes are bank-conflict free too.
 #ifndef DF_TRAIN_SWZ
 #define DF_TRAIN_SWZ 1
 #endif

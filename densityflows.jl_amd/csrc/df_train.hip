@@ -125,7 +125,10 @@ unsigned blocks_for(int64_t count, int threads) { return (unsigned)((count + thr
 
 size_t train_net_lds(int ht, const GNet& g) {
     const size_t tarea = (size_t)kTrainWaves * 2 * 16 * ht * kTS * 4;
-    const size_t red = (size_t)g.p_count * 4;
+    // the reduction: the net's trainables + dW0 / dW1 / dW_out in padded regions
+    // (train_net_kernel; generous bounds: n_in, n_out <= 16, dW1 rows <= h + 8 apart)
+    const size_t h = (size_t)g.h_true;
+    const size_t red = (((size_t)g.p_count + 3) + (h + 1) * 16 + 3 + h * (h + 8) + 3 + 17 * h) * 4;
     if (g.split) return (size_t)g.sfwd_bytes + ht * 1024 + g.st_bytes + (tarea > red ? tarea : red);
     return (size_t)g.fwd_bytes + g.t_bytes + (tarea > red ? tarea : red);
 }

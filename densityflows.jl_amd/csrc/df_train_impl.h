@@ -89,30 +89,34 @@ __device__ __forceinline__ void mul_act_grad(int act, const f32x4 (&y)[HT], f32x
 }
 
 // Column-quad swizzle of the transpose buffers: quad q of row R is stored at quad
-// q ^ tswz(R >> 2), tswz(Q) = the Gray bit of Q & 3 (0, 1, 1, 0).  With the 20-float
-// rows, a b128 read of (row j, quad g) then lands on 16 distinct 4-bank groups in every
-// 16-lane group of ds_read_b128 (a search over all row swizzles); the b32
-// row writes keep their bank sets (a permutation inside the row).
+// q ^ rswz(R), rswz(R) = the Gray bit of (R >> 2) & 3 (0, 1, 1, 0) ^ bit 4 of R.  With
+// the 20-float rows, both b128 read shapes, (row 16m + j, quad g) and the M4 operands'
+// (row lane, quad q), land on 16 distinct 4-bank groups in every 16-lane group of
+// ds_read_b128 (a search over row swizzles; the Gray bit alone leaves the
+// second shape 2-way); the b32 row writes keep their bank sets (a permutation inside
+// the row).
 __device__ __forceinline__ int tswz(int q) { return DF_TRAIN_SWZ ? ((q ^ (q >> 1)) & 1) : 0; }
+__device__ __forceinline__ int rswz(int row) { return DF_TRAIN_SWZ ? (tswz(row >> 2) ^ ((row >> 4) & 1)) : 0; }
 // element (row, col) of a transpose buffer
 __device__ __forceinline__ int tidx(int row, int col) {
-    return row * kTS + ((((col >> 2) ^ tswz(row >> 2)) << 2) | (col & 3));
+    return row * kTS + ((((col >> 2) ^ rswz(row)) << 2) | (col & 3));
 }
 // f32x4 fragment (row, quad q) of a transpose buffer
 __device__ __forceinline__ f32x4 tread(const float* T, int row, int q) {
-    return *reinterpret_cast<const f32x4*>(T + row * kTS + ((q ^ tswz(row >> 2)) << 2));
+    return *reinterpret_cast<const f32x4*>(T + row * kTS + ((q ^ rswz(row)) << 2));
 }
 
 // accumulator-layout tile (rows 16m + 4g + r of sample j) → T[row][j]; the row's
-// quad swizzle is tswz(g) for every (m, r), so the lane's column is loop-invariant
+// quad swizzle is tswz(g) ^ (m & 1) for every r, so the lane's column is fixed per m
 template <int HT>
 __device__ __forceinline__ void t_write(float* T, const f32x4 (&v)[HT]) {
     const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
-    const int col = (((j >> 2) ^ tswz(g)) << 2) | (j & 3);
 #pragma unroll
-    for (int m = 0; m < HT; ++m)
+    for (int m = 0; m < HT; ++m) {
+        const int col = (((j >> 2) ^ (DF_TRAIN_SWZ ? tswz(g) ^ (m & 1) : 0)) << 2) | (j & 3);
 #pragma unroll
         for (int r = 0; r < 4; ++r) T[(16 * m + 4 * g + r) * kTS + col] = v[m][r];
+    }
 }
 
 __device__ __forceinline__ float hsum4(f32x4 v) { return (v[0] + v[1]) + (v[2] + v[3]); }
@@ -532,7 +536,18 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
     // ---- workgroup reduction (fixed wave order) → partial[blockIdx.x] ----
     __syncthreads();
     float* R = tarea;
-    for (int i = tid; i < G.p_count; i += kTrainThreads) R[i] = 0.f;
+    // The weight matrices are summed in regions of their own: in the column-major flat
+    // layout the columns of a lane group share banks (16-way on dW1's read-add-writes,
+    // 4-way on the M4 blocks).  dW0, dW_out: odd column strides (h | 1, n_out | 1); dW1:
+    // row-major with rows P ≡ 4 (mod 8) floats apart, so the two row quads of a 32-lane
+    // group (4g apart) land 16 banks apart and its 16 columns on the rest: conflict-free.
+    // The final copy gathers them back into the flat order.
+    const int hp = G.h_true | 1, sp = N.n_out | 1, P1 = ((G.h_true + 3) & ~7) + 4;
+    float* R0 = R + ((G.p_count + 3) & ~3);
+    float* R1 = R0 + ((hp * G.n_in + 3) & ~3);
+    float* R2 = R1 + ((NH == 1 ? G.h_true * P1 : 0) + 3 & ~3);
+    const int rn = (int)(R2 - R) + sp * G.h_true;
+    for (int i = tid; i < rn; i += kTrainThreads) R[i] = 0.f;
 #pragma unroll
     for (int m = 0; m < HT; ++m) gb0[m] = uni::xgroup_sum(gb0[m]);
 #pragma unroll
@@ -548,9 +563,9 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
             if constexpr (M4) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    if (i < N.n_out && lane < h) R[wo2 + i + N.n_out * lane] += gWo4[i];
+                    if (i < N.n_out && lane < h) R2[i + sp * lane] += gWo4[i];
                     const int row = 4 * (lane >> 2) + i, col = lane & 3;
-                    if (row < h && col < G.n_in) R[wo0 + row + h * col] += gW04[i];
+                    if (row < h && col < G.n_in) R0[row + hp * col] += gW04[i];
                 }
                 if (G.b_off[0] >= 0 && lane < h) R[bo0 + lane] += gb0l;
                 if (g == 0 && G.b_off[2] >= 0 && j < N.n_out) R[bo2 + j] += gbo;
@@ -560,9 +575,9 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int row = 16 * m + 4 * g + r;
-                        if (row < h && j < G.n_in) R[wo0 + row + h * j] += gW0[m][r];
+                        if (row < h && j < G.n_in) R0[row + hp * j] += gW0[m][r];
                         const int ob = 16 * m + j;  // output Dense: row o = 4g + r, column ob
-                        if (4 * g + r < N.n_out && ob < h) R[wo2 + (4 * g + r) + N.n_out * ob] += gWo[m][r];
+                        if (4 * g + r < N.n_out && ob < h) R2[(4 * g + r) + sp * ob] += gWo[m][r];
                     }
                 if (g == 0) {
 #pragma unroll
@@ -579,7 +594,7 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int row = 16 * ma + 4 * g + r, col = 16 * mb + j;
-                            if (row < h && col < h) R[wo1 + row + h * col] += gWh[ma][mb][r];
+                            if (row < h && col < h) R1[col + P1 * row] += gWh[ma][mb][r];
                         }
                 if (g == 0) {
 #pragma unroll
@@ -591,7 +606,21 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
         __syncthreads();
     }
     float* dst = a.partial + (int64_t)blockIdx.x * a.p_total + G.p_begin;
-    for (int i = tid; i < G.p_count; i += kTrainThreads) dst[i] = R[i];
+    for (int i = tid; i < G.p_count; i += kTrainThreads) {
+        const int k0 = i - wo0, k1 = i - wo1, k2 = i - wo2;
+        float v = R[i];
+        if (k0 >= 0 && k0 < h * G.n_in) {
+            const int col = k0 / h;
+            v = R0[(k0 - col * h) + hp * col];
+        } else if (NH == 1 && k1 >= 0 && k1 < h * h) {
+            const int col = k1 / h;
+            v = R1[col + P1 * (k1 - col * h)];
+        } else if (k2 >= 0 && k2 < N.n_out * h) {
+            const int col = k2 / N.n_out;
+            v = R2[(k2 - col * N.n_out) + sp * col];
+        }
+        dst[i] = v;
+    }
 }
 
 template <int HT, int NH, int AM, bool SPLIT = false>
