@@ -517,7 +517,8 @@ def test_split_variant_accuracy(cuda, name, monkeypatch):
     is within 1.5× that of the exact-f32 MFMA kernel (DF_F32_EXACT=1) at the
     median and the 99th percentile, for x and ldj in both directions; the worst
     (ill-conditioned) element within 2× the worst of the exact-f32 kernel and of
-    Flux's op order in fp32."""
+    Flux's op order in fp32, and — against the exact-f32 kernel alone — the
+    99.9th percentile within 2× and the worst element within 3× or under 1e-5."""
     th = None
     if name in ("cfg2", "cfg4"):
         spec, g, meta = G.load(name)
@@ -546,7 +547,7 @@ def test_split_variant_accuracy(cuda, name, monkeypatch):
         x, lf = dfa.forward(chain, _t(z, cuda), tth)
         zb, lb = dfa.backward(chain, _t(xin, cuda), tth)
         res[exact] = [_np(v) for v in (x, lf, zb, lb)]
-    print(f"strict relative error vs fp64 ({name}): quantity split(median, p99, max) | exact-f32(same)")
+    print(f"strict relative error vs fp64 ({name}): quantity split(median, p99, p99.9, max) | exact-f32(same)")
     for i, (key, truth) in enumerate((("x", xo), ("ldj", lo), ("z", zo), ("ldj_bwd", lbo))):
         es = strict_rel(res["0"][i], truth)
         ee = strict_rel(res["1"][i], truth)
@@ -554,7 +555,8 @@ def test_split_variant_accuracy(cuda, name, monkeypatch):
         m = a > 1e-3
         med_s = float(np.median(np.abs(res["0"][i].astype(np.float64) - truth)[m] / a[m]))
         med_e = float(np.median(np.abs(res["1"][i].astype(np.float64) - truth)[m] / a[m]))
-        print(f"  {key}: ({med_s:.3g}, {es[2]:.3g}, {es[0]:.3g}) | ({med_e:.3g}, {ee[2]:.3g}, {ee[0]:.3g})")
+        print(f"  {key}: ({med_s:.3g}, {es[2]:.3g}, {es[1]:.3g}, {es[0]:.3g}) | "
+              f"({med_e:.3g}, {ee[2]:.3g}, {ee[1]:.3g}, {ee[0]:.3g})")
         # the worst element is an ill-conditioned sample whose error depends on the
         # summation order: judged, as in test_strict_elementwise_relative_error, against
         # 2× the worst of the exact-f32 kernel and of Flux's own op order in fp32
@@ -562,6 +564,12 @@ def test_split_variant_accuracy(cuda, name, monkeypatch):
         assert med_s <= 1.5 * med_e + 1e-8, (key, med_s, med_e)
         assert es[2] <= 1.5 * ee[2] + 1e-8, (key, es, ee)
         assert es[0] <= max(1e-5, 2.0 * max(ee[0], ef[0])), (key, es, ee, ef)
+        # SPLIT-specific tail bounds, against the exact-f32 kernel alone (a regression of
+        # the split cannot hide under the worst element of Flux's fp32 op order): the
+        # 99.9th percentile within 2x, the worst element within 3x or under 1e-5
+        # (round 2: worst ratios 2.2x on fast_h32 ldj_bwd, 6.2x on cfg2 ldj at 4.3e-6)
+        assert es[1] <= 2.0 * ee[1] + 1e-8, (key, es, ee)
+        assert es[0] <= max(1e-5, 3.0 * ee[0]), (key, es, ee)
 
 
 @pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4"])
