@@ -211,6 +211,15 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
 
         // ---- epilogue: rows 16m + 4g + q of sample smp[t] ----
         if constexpr (EPI == LEPI_DACT || EPI == LEPI_DACT_XBAR) {
+#if DF_LDENSE_DIAG == 1  // timing diagnostic (wrong results): δ stored without σ' or x̄
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+                if (valid[t])
+#pragma unroll
+                    for (int m = 0; m < MT; ++m)
+                        *reinterpret_cast<f32x4*>(a.out + smp[t] * a.ld_out + 16 * m + 4 * g) = acc[t][m];
+            if (true) continue;
+#endif
 #pragma unroll
             for (int t = 0; t < T; ++t) {
                 // the σ' arguments of the whole tile are loaded at once (a padding
