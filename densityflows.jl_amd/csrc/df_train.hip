@@ -8,11 +8,21 @@ namespace df {
 
 namespace {
 
-void* train_ptr(int ht, int nh, int am, bool split = false) {
+#ifndef DF_TRAIN_NAF
+#define DF_TRAIN_NAF 1
+#endif
+// naf: the transformed-dim count; the SPLIT instances for 2 and 3 (d = 5 chains) have it
+// at compile time (DF_TRAIN_NAF)
+void* train_ptr(int ht, int nh, int am, bool split = false, int naf = 0) {
     if (split) {
         if (nh != 1 || am != trn::AM_RELU) return nullptr;
-        if (ht == 2) return train_kernel_ptr<2, 1, trn::AM_RELU, true>();
-        if (ht == 4) return train_kernel_ptr<4, 1, trn::AM_RELU, true>();
+        const int nf = DF_TRAIN_NAF ? naf : 0;
+        if (ht == 2) return nf == 2 ? train_kernel_ptr<2, 1, trn::AM_RELU, true, 2>()
+                            : nf == 3 ? train_kernel_ptr<2, 1, trn::AM_RELU, true, 3>()
+                                      : train_kernel_ptr<2, 1, trn::AM_RELU, true>();
+        if (ht == 4) return nf == 2 ? train_kernel_ptr<4, 1, trn::AM_RELU, true, 2>()
+                            : nf == 3 ? train_kernel_ptr<4, 1, trn::AM_RELU, true, 3>()
+                                      : train_kernel_ptr<4, 1, trn::AM_RELU, true>();
         return nullptr;
     }
 #define DF_T(H)                                                                                           \
@@ -142,16 +152,19 @@ hipError_t set_train_lds_limit(size_t lds) {
                 if (e != hipSuccess) return e;
             }
     for (int ht : {2, 4}) {
-        hipError_t e = hipFuncSetAttribute(train_ptr(ht, 1, trn::AM_RELU, true),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
+        for (int naf : {0, 2, 3}) {
+            hipError_t e = hipFuncSetAttribute(train_ptr(ht, 1, trn::AM_RELU, true, naf),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
     }
     return hipSuccess;
 }
 
 hipError_t launch_train_net(int ht, int nh, int am, const TrainArgs& a, unsigned grid, size_t lds,
                             hipStream_t st) {
-    void* k = train_ptr(ht, nh, am, a.net.split != 0);
+    const int naf = (a.net.split && a.net.su.n_out == a.n_af) ? a.n_af : 0;  // out_valu<NO = NAF> needs n_out = n_af
+    void* k = train_ptr(ht, nh, am, a.net.split != 0, naf);
     if (!k) return hipErrorInvalidValue;
     void* args[] = {const_cast<TrainArgs*>(&a)};
     return hipLaunchKernel(k, dim3(grid), dim3(kTrainThreads), args, lds, st);

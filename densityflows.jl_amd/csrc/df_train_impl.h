@@ -155,9 +155,12 @@ __device__ __forceinline__ f32x4 mfma4x4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
 
-template <int HT, int NH, int AM, bool SPLIT = false>
+// NAF > 0: the transformed-dim count (= output count) at compile time (SPLIT instances,
+// 2 and 3: the d = 5 chains); 0: a.n_af at run time.
+template <int HT, int NH, int AM, bool SPLIT = false, int NAF = 0>
 __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a) {
     using namespace trn;
+    const int n_af = NAF > 0 ? NAF : a.n_af;
     constexpr bool RELU = (AM == AM_RELU);
     constexpr bool PRE = (AM == AM_PRE);
     constexpr bool M4 = SPLIT && DF_TRAIN_M4;
@@ -233,7 +236,7 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
         const int f = 4 * g + r;
         const int fs = (f < G.n_in) ? a.feat[f] : -1;
         zxp8 |= (uint32_t)((fs >= n && fs < n + d) ? fs - n : 0xff) << (8 * r);
-        afp8 |= (uint32_t)((r < a.n_af) ? a.af[r] - n : 0xff) << (8 * r);
+        afp8 |= (uint32_t)((r < n_af) ? a.af[r] - n : 0xff) << (8 * r);
     }
     // per-iteration opaque copies of the tables (refreshed at each tile start): the
     // compiler must not hoist 64-bit addresses derived from them out of the tile loop
@@ -337,7 +340,7 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
         f32x4 o[1];
         float dfo[4] = {1.f, 1.f, 1.f, 1.f};  // AM_PRE: σo'(pre) of the output Dense
         if constexpr (PRE) {
-            uni::out_valu<HT, 1, true>(fw, N, H, o);  // pre-activation (no σo)
+            uni::out_valu<HT, 1, true, NAF>(fw, N, H, o);  // pre-activation (no σo)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float x = o[0][k];
@@ -346,7 +349,7 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
                 o[0][k] = y;
             }
         } else {
-            uni::out_valu<HT, 1, RELU>(fw, N, H, o);
+            uni::out_valu<HT, 1, RELU, NAF>(fw, N, H, o);
         }
 
         // ---- coupling pullback → ȳ (every lane group holds all outputs of sample j) ----
@@ -356,7 +359,7 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
             dout[k] = 0.f;
             zb[k] = 0.f;
             ee[k] = 1.f;
-            if (k < a.n_af && valid) {
+            if (k < n_af && valid) {
                 zb[k] = zbp[k];
                 if (sph) {
                     ee[k] = expf(-o[0][k]);
@@ -375,7 +378,7 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
         if (sph && g == 0 && valid) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (k < a.n_af) a.ebuf[s * 4 + k] = ee[k];
+                if (k < n_af) a.ebuf[s * 4 + k] = ee[k];
         }
 
         // ---- output Dense: dW3 += ȳ·hᵀ, db3 += Σȳ, h̄ = W3ᵀ ȳ ----
@@ -413,7 +416,7 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
         for (int m = 0; m < HT; ++m) hb[0][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (k < a.n_af) {
+            if (k < n_af) {
 #pragma unroll
                 for (int m = 0; m < HT; ++m) {
                     const f32x4 w = impl::lds4(fw + N.off_out + ((k * INP + 16 * m + 4 * g) << 2));
@@ -623,9 +626,9 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
     }
 }
 
-template <int HT, int NH, int AM, bool SPLIT = false>
+template <int HT, int NH, int AM, bool SPLIT = false, int NAF = 0>
 void* train_kernel_ptr() {
-    return reinterpret_cast<void*>(&train_net_kernel<HT, NH, AM, SPLIT>);
+    return reinterpret_cast<void*>(&train_net_kernel<HT, NH, AM, SPLIT, NAF>);
 }
 
 }  // namespace df
