@@ -163,7 +163,8 @@ hipError_t set_train_lds_limit(size_t lds) {
 
 hipError_t launch_train_net(int ht, int nh, int am, const TrainArgs& a, unsigned grid, size_t lds,
                             hipStream_t st) {
-    const int naf = (a.net.split && a.net.su.n_out == a.n_af) ? a.n_af : 0;  // out_valu<NO = NAF> needs n_out = n_af
+    // out_valu<NO = NAF> needs n_out = n_af, the 4x4x1 x̄ at most 4 conditioner inputs
+    const int naf = (a.net.split && a.net.su.n_out == a.n_af && a.net.n_in <= 4) ? a.n_af : 0;
     void* k = train_ptr(ht, nh, am, a.net.split != 0, naf);
     if (!k) return hipErrorInvalidValue;
     void* args[] = {const_cast<TrainArgs*>(&a)};

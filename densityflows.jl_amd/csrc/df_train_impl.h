@@ -156,7 +156,8 @@ __device__ __forceinline__ f32x4 mfma4x4(float a, float b, f32x4 c) {
 }
 
 // NAF > 0: the transformed-dim count (= output count) at compile time (SPLIT instances,
-// 2 and 3: the d = 5 chains); 0: a.n_af at run time.
+// 2 and 3: the d = 5 chains; the launcher also requires ≤ 4 conditioner inputs);
+// 0: a.n_af at run time.
 template <int HT, int NH, int AM, bool SPLIT = false, int NAF = 0>
 __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a) {
     using namespace trn;
@@ -517,11 +518,28 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
             }
         }
         f32x4 xb = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (NAF > 0) {
+            // ≤ 4 features (the launcher's condition for these instances): x̄ on
+            // v_mfma_f32_4x4x1_16b_f32 instead of a 16-row product with ≤ 4 live rows.
+            // Block b = lane >> 2 takes samples 4(b & 3).. over the hidden rows of lane
+            // group g = b >> 2 — exactly the δ0 values lane (g, j) holds — with W0ᵀ[i][h]
+            // from the fragment of lane (g, i); the four groups' partial sums are then
+            // added across lane groups.  Lane (g, j) ends with x̄[f][j] in register f.
 #pragma unroll
-        for (int kq = 0; kq < HT; ++kq) {
-            const f32x4 w = impl::lds4(tw + G.off_w0t + kq * 1024 + lane * 16);
+            for (int kq = 0; kq < HT; ++kq) {
+                const f32x4 w = impl::lds4(tw + G.off_w0t + kq * 1024 + (lane & 0x33) * 16);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) xb = mfma4(w[r], d0[0][kq][r], xb);
+                for (int r = 0; r < 4; ++r) xb = mfma4x4(w[r], d0[0][kq][r], xb);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xb[r] = uni::xgroup_sum(xb[r]);
+        } else {
+#pragma unroll
+            for (int kq = 0; kq < HT; ++kq) {
+                const f32x4 w = impl::lds4(tw + G.off_w0t + kq * 1024 + lane * 16);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xb = mfma4(w[r], d0[0][kq][r], xb);
+            }
         }
         if (valid) {
 #pragma unroll
