@@ -80,6 +80,7 @@ struct LDenseArgs {
     // LEPI_DACT_XBAR: x̄ = W0ᵀ δ0 right after δ0 (fragments resident in LDS)
     const uint8_t* w0t;
     int w0t_mt, w0t_nkq;
+    const uint8_t* w0s;     // SPLIT instances: W0ᵀ as bf16x3 planes [c][m][p][lane][8] (x̄ on bf16 MFMA), or nullptr
     // couple_bwd_kernel: second product W_outᵀ ȳ (fragments [kq][m][lane][4], m < 16·HT rows)
     const uint8_t* w2frag;
     int nkq2;

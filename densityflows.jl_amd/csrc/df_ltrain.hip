@@ -64,8 +64,9 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
     // after the chunk buffer(s): two full chunks, or the single (possibly short) one
     uint8_t* w0t_lds = smem + (nchunks > 1 ? 2 * chunk_bytes : SPLIT ? chunk_bytes : a.nkq * MT * 1024);
     if constexpr (EPI == LEPI_DACT_XBAR) {  // W0ᵀ fragments stay resident for the x̄ product
-        const int n16 = a.w0t_mt * a.w0t_nkq * 64;
-        const f32x4* src = reinterpret_cast<const f32x4*>(a.w0t);
+        // f32 fragments, or (SPLIT, a.w0s) bf16x3 planes [c][m][p][lane][8] of 32-row chunks
+        const int n16 = (SPLIT && a.w0s) ? (a.w0t_nkq / 2) * a.w0t_mt * 3 * 64 : a.w0t_mt * a.w0t_nkq * 64;
+        const f32x4* src = reinterpret_cast<const f32x4*>((SPLIT && a.w0s) ? a.w0s : a.w0t);
         for (int q = threadIdx.x; q < n16; q += kBlockThreads) reinterpret_cast<f32x4*>(w0t_lds)[q] = src[q];
         // z̄ column of conditioner feature f (0xff: not an identity dim of z; d <= 64),
         // 64 bytes after the W0ᵀ fragments, fixed for the launch
@@ -250,7 +251,8 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
                     // The z̄ entries it adds to are read ahead of the product (their latency
                     // overlaps its MFMAs), all loads ahead of all stores: distinct features
                     // of a sample map to distinct state slots (axis_nn).
-                    const uint8_t* zcol = w0t_lds + a.w0t_mt * a.w0t_nkq * 1024;
+                    const uint8_t* zcol = w0t_lds + ((SPLIT && a.w0s) ? (a.w0t_nkq / 2) * a.w0t_mt * 3072
+                                                                       : a.w0t_mt * a.w0t_nkq * 1024);
                     uint32_t zoff[4];  // the columns of features 16m + 4g + q, a byte per q
                     float zv[4][4];
 #pragma unroll
@@ -267,6 +269,36 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
                     f32x4 xb[4];
 #pragma unroll
                     for (int m = 0; m < 4; ++m) xb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if (SPLIT && a.w0s) {
+                        // bf16x3 split products on bf16 MFMA: δ0's accumulator tiles 2c, 2c+1 are
+                        // one B operand (k = 32c + 16(e>>2) + 4g + (e&3), the W1ᵀ planes' order)
+#pragma unroll
+                        for (int c = 0; c < MT / 2; ++c) {
+                            if (2 * c < a.w0t_nkq) {
+                                const float v[8] = {acc[t][2 * c][0],     acc[t][2 * c][1],     acc[t][2 * c][2],
+                                                    acc[t][2 * c][3],     acc[t][2 * c + 1][0], acc[t][2 * c + 1][1],
+                                                    acc[t][2 * c + 1][2], acc[t][2 * c + 1][3]};
+                                uni::bf16x8 x0, x1, x2;
+                                uni::split8(v, x0, x1, x2);
+#pragma unroll
+                                for (int m = 0; m < 4; ++m) {
+                                    if (m < a.w0t_mt) {
+                                        const uint8_t* wp = w0t_lds + (c * a.w0t_mt + m) * 3072 + lane * 16;
+                                        const uni::bf16x8 w0 = *reinterpret_cast<const uni::bf16x8*>(wp);
+                                        const uni::bf16x8 w1 = *reinterpret_cast<const uni::bf16x8*>(wp + 1024);
+                                        const uni::bf16x8 w2 = *reinterpret_cast<const uni::bf16x8*>(wp + 2048);
+                                        f32x4 u = xb[m];  // small terms first
+                                        u = uni::mfma_bf(w2, x0, u);
+                                        u = uni::mfma_bf(w1, x1, u);
+                                        u = uni::mfma_bf(w0, x2, u);
+                                        u = uni::mfma_bf(w1, x0, u);
+                                        u = uni::mfma_bf(w0, x1, u);
+                                        xb[m] = uni::mfma_bf(w0, x0, u);
+                                    }
+                                }
+                            }
+                        }
+                    } else
 #pragma unroll
                     for (int kq = 0; kq < MT; ++kq) {
                         if (kq < a.w0t_nkq) {

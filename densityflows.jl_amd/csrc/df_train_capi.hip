@@ -211,8 +211,10 @@ LOp pack_lop(df_train* t, const Plan& P, const LDense& D, bool transposed) {
                     t->ldst.push_back((int32_t)(f0 + q));
                     t->lsrc.push_back((int32_t)src);
                 }
-    // SPLIT planes of a hidden-256 Wᵀ (the ldense_kernel SPLIT instances)
-    if (transposed && op.mt == 16 && op.nkq % 2 == 0 && !t->c->exact) {
+    // SPLIT planes of a hidden-256 Wᵀ (the ldense_kernel SPLIT instances), and of a first
+    // Dense's W0ᵀ over a 256-wide hidden layer (≤ 64 conditioner inputs: the x̄ product
+    // of the SPLIT W1ᵀδ1 epilogue)
+    if (transposed && (op.mt == 16 || (op.mt <= 4 && op.nkq == 16)) && op.nkq % 2 == 0 && !t->c->exact) {
         op.sfrag = (int64_t)t->lsblob.size();
         t->lsblob.resize(t->lsblob.size() + (size_t)(op.nkq / 2) * op.mt * 3072, 0);
         for (int c = 0; c < op.nkq / 2; ++c)
@@ -728,10 +730,15 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
                     const LOp& lo = N.dn[k].bwd;
                     const int nchunks = (lo.nkq + lo.chunk_kq - 1) / lo.chunk_kq;
                     c2.sfrag = sfrag_of(lo, LIN_BUF, LEPI_DACT_XBAR);
+                    // x̄ on split products when the W1ᵀδ1 product is SPLIT and W0ᵀ has planes
+                    c2.w0s = (c2.sfrag && N.dn[0].bwd.sfrag >= 0 && c2.w0t_nkq <= 16) ? lsb + N.dn[0].bwd.sfrag
+                                                                                     : nullptr;
                     const size_t wbytes = c2.sfrag ? (size_t)(lo.nkq / 2 > 1 ? 2 : 1) * lo.mt * 3072
                                                    : (size_t)(nchunks > 1 ? 2 : 1) * std::min(lo.nkq, lo.chunk_kq) *
                                                          lo.mt * 1024;
-                    const size_t lds2 = wbytes + (size_t)c2.w0t_mt * c2.w0t_nkq * 1024 + 64;  // + z̄ column table
+                    const size_t w0b = c2.w0s ? (size_t)(c2.w0t_nkq / 2) * c2.w0t_mt * 3072
+                                              : (size_t)c2.w0t_mt * c2.w0t_nkq * 1024;
+                    const size_t lds2 = wbytes + w0b + 64;  // + z̄ column table
                     c2.wfrag = lb + lo.frag;
                     c2.nkq = lo.nkq;
                     c2.chunk_kq = lo.chunk_kq;
