@@ -3,12 +3,14 @@
 # (and a longer run), every secondary workload, kernel traces (the driver's exact command
 # included) and PMC passes (tools/pmc_sets.txt, one counter set per run) of the forward
 # and training kernels.  Collected into profiles/ by tools/collect_profiles.py.
+# NOPMC=1: everything but the PMC passes; PMCONLY=1: the PMC passes alone.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r3}
 mkdir -p $O
 python3 -c "import bench; print(bench.source_sha16())" > $O/source_sha16.txt
+if [ "${PMCONLY:-0}" != 1 ]; then  # PMCONLY=1: the PMC passes alone (a second call)
 timeout -k 10 900 python -u -m pytest tests -m gpu -v -rs --timeout 180 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc $rc" >> $O/pytest_gpu.log
@@ -32,6 +34,7 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
     python3 bench.py --mode train --steps 10 --warmup 3 > $O/prof_t2.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_t5 -o run -- \
     python3 bench.py --mode train --config cfg4 --steps 3 --warmup 1 > $O/prof_t5.log 2>&1 || exit 1
+fi
 [ "${NOPMC:-0}" = 1 ] && exit 0
 i=0
 for cfg in cfg2 cfg4; do
