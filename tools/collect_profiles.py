@@ -33,7 +33,8 @@ PMC = [
     ("pmc_cfg2", "cfg2 forward, FAST SPLIT kernel", [("uniform_kernel<4, 0", None)]),
     ("pmc_cfg4", "cfg4 forward, wide SPLIT kernel", [("wide_kernel<0", None)]),
     ("pmct_cfg2", "config-2 train step (bench --mode train)",
-     [("train_net_kernel<4, 1, 1, true>", "train_net_kernel<4, 1, 1, true>"),
+     [("train_net_kernel<4, 1, 1, true, 3>", "train_net_kernel<4, 1, 1, true, 3> (3-output nets)"),
+      ("train_net_kernel<4, 1, 1, true, 2>", "train_net_kernel<4, 1, 1, true, 2> (2-output nets)"),
       ("uniform_kernel<4, 3", "uniform_kernel<4, 3, true, true, true, true>")]),
     ("pmct_cfg4", "config-5 train step (bench --mode train --config cfg4)",
      [("sweep_kernel<16, 1>", "sweep_kernel<16, 1>"), ("wide_kernel<3, true>", "wide_kernel<3, true>"),
