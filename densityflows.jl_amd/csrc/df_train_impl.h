@@ -190,7 +190,18 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
         const f32x4* src = reinterpret_cast<const f32x4*>(SPLIT ? a.sblob + G.sfwd_src : a.blob + G.fwd_src);
         for (int i = tid; i < fwd_bytes / 16; i += kTrainThreads) reinterpret_cast<f32x4*>(fw)[i] = src[i];
         const f32x4* srt = reinterpret_cast<const f32x4*>(a.tblob + G.t_src);
-        for (int i = tid; i < t_bytes / 16; i += kTrainThreads) reinterpret_cast<f32x4*>(tw)[i] = srt[i];
+        if constexpr (NAF > 0) {
+            // W0ᵀ alone (SPLIT), read only by the 4x4x1 x̄, which takes the fragments of lanes
+            // (lane & 3) + 16g: those 16 per k-quad go to slots (lane & 3) + 4g, one 256-byte
+            // run (its ds_read_b128 then hit 16 distinct bank groups instead of 4)
+            const int w0 = G.off_w0t / 16;
+            for (int i = tid; i < HT * 16; i += kTrainThreads) {
+                const int kq = i >> 4, c = i & 15;
+                reinterpret_cast<f32x4*>(tw)[w0 + kq * 64 + c] = srt[w0 + kq * 64 + (c & 3) + 16 * (c >> 2)];
+            }
+        } else {
+            for (int i = tid; i < t_bytes / 16; i += kTrainThreads) reinterpret_cast<f32x4*>(tw)[i] = srt[i];
+        }
         if constexpr (SPLIT) {
             const f32x4* sst = reinterpret_cast<const f32x4*>(a.tsblob + G.st_src);
             for (int i = tid; i < G.st_bytes / 16; i += kTrainThreads) reinterpret_cast<f32x4*>(stw)[i] = sst[i];
@@ -523,11 +534,12 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
             // v_mfma_f32_4x4x1_16b_f32 instead of a 16-row product with ≤ 4 live rows.
             // Block b = lane >> 2 takes samples 4(b & 3).. over the hidden rows of lane
             // group g = b >> 2 — exactly the δ0 values lane (g, j) holds — with W0ᵀ[i][h]
-            // from the fragment of lane (g, i); the four groups' partial sums are then
-            // added across lane groups.  Lane (g, j) ends with x̄[f][j] in register f.
+            // from the fragment of lane (g, i), i < 4 (at slot i + 4g: the LDS copy compacts
+            // them); the four groups' partial sums are then added across lane groups.
+            // Lane (g, j) ends with x̄[f][j] in register f.
 #pragma unroll
             for (int kq = 0; kq < HT; ++kq) {
-                const f32x4 w = impl::lds4(tw + G.off_w0t + kq * 1024 + (lane & 0x33) * 16);
+                const f32x4 w = impl::lds4(tw + G.off_w0t + kq * 1024 + ((lane & 3) + 4 * g) * 16);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) xb = mfma4x4(w[r], d0[0][kq][r], xb);
             }
