@@ -156,14 +156,25 @@ def cpu_baseline(chain, d, n, seconds=12.0, sample=65536):
     th = rng.random((n, sample)).astype(np.float32)
     f.forward(z[:, :256], th[:, :256], threads)  # warm-up
     done, t0 = 0, time.perf_counter()
+    win, w0, wdone = [], t0, 0       # per-window rates (~1 s each): the spread within this run
     while True:
         f.forward(z, th, threads)
         done += sample
-        el = time.perf_counter() - t0
+        wdone += sample
+        now = time.perf_counter()
+        if now - w0 >= 1.0:
+            win.append(wdone / (now - w0) / 1e6)
+            w0, wdone = now, 0
+        el = now - t0
         if el >= seconds:
             break
+    win = sorted(win) or [done / el / 1e6]
     return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": int(threads), "kind": "port",
             "cpu_model": cpu_model(),
+            "spread_1s_windows": {"min": round(win[0], 4), "median": round(win[len(win) // 2], 4),
+                                  "max": round(win[-1], 4), "windows": len(win),
+                                  "note": "the host is shared: earlier rounds measured 4.5-7.2 Msamples/s on "
+                                          "identical code across boxes (16 visible cores of a 64-core EPYC)"},
             "sample": f"{done} samples ({done // sample} passes of a {sample}-sample batch, C++/OpenMP fp32 "
                       f"restatement oracle/cpu_flow.cpp, {threads} threads) in {el:.1f} s"}
 
@@ -252,7 +263,8 @@ def main():
     ap.add_argument("--no-exact", action="store_true",
                     help="skip the exact-f32 FAST kernel timing that accompanies a SPLIT-kernel bench")
     ap.add_argument("--no-clock", action="store_true",
-                    help="do not stamp the effective shader clock of the timed launches (df_chain_clock_probe)")
+                    help="skip the clock run: a separate run of launches after the timed loop with the in-kernel "
+                         "clock stamps on (df_chain_clock_probe); the timed launches never carry stamps")
     ap.add_argument("--settle-seconds", type=float, default=0.3,
                     help="untimed steps after the W warm-up steps until this much warm-up time has passed "
                          "(DVFS clock ramp; 0 = exactly W)")
@@ -309,15 +321,23 @@ def main():
 
     trainer = None
     comm = None
+    comm_error = None
     probe = hc                       # the handle whose chain-pass launches carry the clock stamps
     rehearsal = dist is not None and dist.get_backend() != "nccl"   # gloo: ranks may share one GPU
-    if args.mode != "forward" and not rehearsal:
+    if not rehearsal:
         # the library's own RCCL communicator (df_comm) carries every exchange of the
-        # nll / train steps, at every rank count (world 1 included)
+        # nll / train steps, at every rank count (world 1 included).  The forward step has
+        # no exchange; there it only carries the per-rank report after the timed loop, and a
+        # failure to build it is reported in the line instead of ending the run
         from densityflows_amd.parallel import DFComm
 
-        with _stdout_to_stderr():
-            comm = DFComm(gpu, rank, world)
+        try:
+            with _stdout_to_stderr():
+                comm = DFComm(gpu, rank, world)
+        except Exception as e:          # noqa: BLE001
+            if args.mode != "forward":
+                raise
+            comm_error = f"{type(e).__name__}: {e}"
     if args.mode == "forward":
         def step():
             hc.run("forward", zbuf, thbuf, xbuf, ldj, B)
@@ -363,8 +383,6 @@ def main():
     stream = torch.cuda.current_stream(dev)
     steplog = os.environ.get("DF_BENCH_STEPLOG") == "1"   # diagnostic: per-step HIP-event times on stderr
     warm_ms = []
-    if not args.no_clock:
-        probe.clock_probe(True)      # allocates the stamp slots during the warm-up
     t_warm = time.perf_counter()
     for _ in range(args.warmup):
         if steplog:
@@ -387,8 +405,6 @@ def main():
         settle_steps += 8
         torch.cuda.synchronize()
     settle_s = time.perf_counter() - t_w
-    if not args.no_clock:
-        probe.clock_probe(True)      # zero the stamps: they cover exactly the timed launches
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -411,13 +427,27 @@ def main():
     gpu_ms = ev0.elapsed_time(ev1)                 # HIP events on the launch stream
     clock = None
     if not args.no_clock:
+        # the clock run: the same steps right after the timed loop (the chip still at its
+        # steady clock) with the in-kernel stamps on; the timed launches above ran the plain
+        # production kernels
+        k_clk = min(max(args.steps, 1), 50)
+        probe.clock_probe(True)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
+        for _ in range(k_clk):
+            step()
+        c1.record(stream)
+        torch.cuda.synchronize()
+        clk_ms = c0.elapsed_time(c1) / k_clk
         ghz_med, ghz_mean, slots = probe.clock_read()
         probe.clock_probe(False)
         if slots > 0:
             clock = {"ghz_median": round(ghz_med, 4), "ghz_sum_ratio": round(ghz_mean, 4), "workgroup_slots": slots,
-                     "kernel_mcycles_per_launch": None,
-                     "source": "in-kernel s_memtime / s_memrealtime (100 MHz) stamps by wave 0 of every workgroup of "
-                               "the timed chain-pass launches (df_chain_clock_probe)"}
+                     "kernel_mcycles_per_launch": None, "clock_run_steps": k_clk,
+                     "clock_run_ms_per_step": round(clk_ms, 4),
+                     "source": "in-kernel s_memtime / s_memrealtime (100 MHz) stamps by wave 0 of every workgroup, "
+                               "taken in a separate run of clock_run_steps launches right after the timed loop "
+                               "(df_chain_clock_probe); the timed launches carry no stamps"}
     if steplog:
         print(json.dumps({"rank": rank, "warmup_ms": [round(a.elapsed_time(b), 4) for a, b in warm_ms],
                           "step_ms": [round(step_ev[i].elapsed_time(step_ev[i + 1]), 4) for i in range(args.steps)]}),
@@ -426,12 +456,15 @@ def main():
     if dist is not None:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
+    ranks = rank_report(dist, dev, gpu_ms / args.steps, wall * 1e3 / args.steps, world, B, comm, comm_error,
+                        "torch.distributed " + (dist.get_backend() if dist is not None else "none"))
     total = B * world * args.steps
     value = total / elapsed / 1e6
     kernel_s = gpu_ms / 1e3 / args.steps            # mean launch time (one launch per step)
     if clock is not None and args.mode != "train":
-        # clock-normalised time: shader cycles per launch (comparable across boxes and DVFS states)
-        clock["kernel_mcycles_per_launch"] = round(kernel_s * clock["ghz_median"] * 1e3, 4)
+        # clock-normalised time: shader cycles per launch of the clock run (comparable across
+        # boxes and DVFS states)
+        clock["kernel_mcycles_per_launch"] = round(clock["clock_run_ms_per_step"] * clock["ghz_median"] * 1e3, 4)
     flop = info.flops_per_sample * B
     achieved_tflops = flop / kernel_s / 1e12
     hbm_algo = (8.0 * d + 4.0 * n + 4.0) * B          # read z (+θ), write x, ldj
@@ -525,7 +558,10 @@ def main():
                          "hbm_algorithmic_GBps": round(hbm_algo / kernel_s / 1e9, 2)},
             "clock": clock,
             "clock_settle": {"untimed_steps_after_warmup": settle_steps, "seconds": round(settle_s, 3),
-                             "target_seconds_of_warmup": args.settle_seconds},
+                             "target_seconds_of_warmup": args.settle_seconds,
+                             "policy": "after the W warm-up steps, untimed steps run until settle-seconds of "
+                                       "warm-up have passed (DVFS clock ramp); the K timed steps are unchanged"},
+            "ranks": ranks,
         }
         if args.mode == "train" and clock is not None:
             clock["scope"] = "the inverse chain pass of each step only"
@@ -548,6 +584,39 @@ def main():
         dist.destroy_process_group()
 
 
+def rank_report(dist, dev, kernel_ms, wall_ms, world, batch, comm, comm_error, group_desc):
+    """Per-rank timing spread and the communicator behind the line:
+    every rank's mean kernel (HIP-event) and wall time per step, gathered to rank 0
+    (min / max / per rank); the df_comm size from df_comm_get_info, and one RCCL
+    all-reduce of this rank's sample count through it, checked against B x world.
+    Runs after the timed loop."""
+    import torch
+
+    mine = torch.tensor([kernel_ms, wall_ms], dtype=torch.float64, device=dev)
+    if dist is not None:
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        allv = torch.stack(allv).cpu().tolist()
+    else:
+        allv = [mine.cpu().tolist()]
+    k = [v[0] for v in allv]
+    w = [v[1] for v in allv]
+    out = {"n": len(allv), "kernel_ms_min": round(min(k), 4), "kernel_ms_max": round(max(k), 4),
+           "wall_ms_per_step_min": round(min(w), 4), "wall_ms_per_step_max": round(max(w), 4),
+           "kernel_ms_per_rank": [round(x, 4) for x in k], "process_group": group_desc, "df_comm": None}
+    if comm is not None:
+        r, nr, d = comm.info()
+        cnt = torch.tensor([float(batch), float(nr)], dtype=torch.float64, device=dev)
+        comm.allreduce_(cnt)
+        torch.cuda.synchronize()
+        out["df_comm"] = {"nranks": nr, "rank": r, "device": d,
+                          "allreduce_count_ok": float(cnt[0].item()) == float(batch) * world,
+                          "allreduce_nranks_sum": float(cnt[1].item())}
+    elif comm_error is not None:
+        out["df_comm"] = {"error": comm_error}
+    return out
+
+
 def dry_run(args, world, rank):
     """The bench's launch, rendezvous and max-over-ranks timing without the
     library or a GPU: tests of `--gpus N` self-launching run it on CPU (gloo)."""
@@ -567,13 +636,18 @@ def dry_run(args, world, rank):
         pass
     if dist is not None:
         dist.barrier()
-    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    wall = time.perf_counter() - t0
+    elapsed = torch.tensor([wall], dtype=torch.float64)
     if dist is not None:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    ranks = rank_report(dist, torch.device("cpu"), 0.0, wall * 1e3 / max(args.steps, 1), world, 0, None, None,
+                        "torch.distributed " + (dist.get_backend() if dist is not None else "none"))
+    ranks["group_size"] = dist.get_world_size() if dist is not None else 1
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "Msamples/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "dry_run": True,
-                          "ms_per_step": float(elapsed.item()) * 1e3 / max(args.steps, 1)}), flush=True)
+                          "ms_per_step": float(elapsed.item()) * 1e3 / max(args.steps, 1), "ranks": ranks}),
+              flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

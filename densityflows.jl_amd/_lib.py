@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdensityflows_hip.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # df_status
 DF_OK = 0
@@ -28,6 +28,11 @@ DF_ERR_NONFINITE = -6
 DF_DTYPE_F32 = 0
 DF_DTYPE_F64 = 1
 DF_COMM_ID_BYTES = 128
+
+# df_theta_input (df_train_set_theta_input)
+DF_THETA_AUTO = 0
+DF_THETA_RAW = 1
+DF_THETA_GIVEN = 2
 
 # df_layer_kind
 DF_LAYER_RNVP = 0
@@ -125,6 +130,8 @@ SIGNATURES = {
     "df_flow_forward_inplace": (C.c_int, [_VP, _VP, _VP, _I64, _VP]),
     "df_flow_logpdf": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP]),
     "df_flow_logpdf_sum": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP]),
+    "df_chain_logpdf": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP]),
+    "df_chain_logpdf_sum": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP]),
     "df_train_create": (C.c_int, [C.POINTER(_VP), _VP, C.POINTER(df_adam)]),
     "df_train_destroy": (C.c_int, [_VP]),
     "df_train_num_params": (C.c_int, [_VP, C.POINTER(_I64)]),
@@ -136,6 +143,7 @@ SIGNATURES = {
     "df_train_get_params": (C.c_int, [_VP, _FP, _I64]),
     "df_train_set_params": (C.c_int, [_VP, _FP, _I64]),
     "df_train_set_debug": (C.c_int, [_VP, C.c_int]),
+    "df_train_set_theta_input": (C.c_int, [_VP, C.c_int]),
     "df_chain_set_weights": (C.c_int, [_VP, C.POINTER(df_chain_desc)]),
     "df_comm_get_unique_id": (C.c_int, [_VP]),
     "df_comm_init_rank": (C.c_int, [C.POINTER(_VP), C.c_int, _VP, C.c_int, C.c_int]),
@@ -143,6 +151,7 @@ SIGNATURES = {
     "df_comm_get_info": (C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "df_comm_allreduce_sum": (C.c_int, [_VP, _VP, _I64, C.c_int, _VP]),
     "df_flow_nll": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _VP]),
+    "df_chain_nll": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP, _VP]),
     "df_train_allreduce_gradient": (C.c_int, [_VP, _VP, _VP]),
     "df_train_step_dist": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _I64, _VP, _VP]),
     "df_flow_sample": (C.c_int, [_VP, _VP, _VP, C.c_int, _I64, C.c_uint64, C.c_uint64, _VP]),

@@ -430,7 +430,13 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
         c->partial_gen++;
     }
 
-    if (c->clk_on && grid > c->clk_cap) {  // stamp slots for this grid (zeroed: a new series)
+    // Clock stamps are an eager-launch diagnostic: a launch recorded into a stream
+    // capture (df_train_step_graph) never stamps, so no graph names d_clk and no
+    // allocation runs inside a capture.
+    hipStreamCaptureStatus cap_status = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cap_status) != hipSuccess) cap_status = hipStreamCaptureStatusNone;
+    const bool stamp = c->clk_on && cap_status == hipStreamCaptureStatusNone;
+    if (stamp && grid > c->clk_cap) {  // stamp slots for this grid (zeroed: a new series)
         if (c->d_clk) (void)hipFree(c->d_clk);
         c->d_clk = nullptr;
         c->clk_cap = 0;
@@ -441,7 +447,7 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     }
 
     df::ChainArgs a{};
-    a.clk = c->clk_on ? c->d_clk : nullptr;
+    a.clk = stamp ? c->d_clk : nullptr;
     a.zin = zin;
     a.theta = theta;
     a.xout = xout;
@@ -571,6 +577,18 @@ int df_flow_logpdf_sum(df_chain* c, const float* x, const float* theta_raw, doub
                        void* stream) {
     if (!sum_out) return set_err(DF_ERR_INVALID, "null sum output");
     return run(c, df::MODE_LOGPDF, true, x, theta_raw, nullptr, nullptr, nullptr, sum_out, batch, stream);
+}
+
+int df_chain_logpdf(df_chain* c, const float* x, const float* theta, float* logpdf_out, int64_t batch,
+                    void* stream) {
+    if (batch > 0 && !logpdf_out) return set_err(DF_ERR_INVALID, "null logpdf output");
+    return run(c, df::MODE_LOGPDF, false, x, theta, nullptr, nullptr, logpdf_out, nullptr, batch, stream);
+}
+
+int df_chain_logpdf_sum(df_chain* c, const float* x, const float* theta, double* sum_out, int64_t batch,
+                        void* stream) {
+    if (!sum_out) return set_err(DF_ERR_INVALID, "null sum output");
+    return run(c, df::MODE_LOGPDF, false, x, theta, nullptr, nullptr, nullptr, sum_out, batch, stream);
 }
 
 int df_chain_clock_probe(df_chain* c, int on) {

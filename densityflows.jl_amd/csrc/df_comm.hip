@@ -185,13 +185,19 @@ int df_comm_allreduce_sum(df_comm* c, void* buf, int64_t count, int dtype, void*
     return e == ncclSuccess ? DF_OK : nccl_err(r, e, "ncclAllReduce");
 }
 
-int df_flow_nll(df_chain* chain, df_comm* comm, const float* x, const float* theta_raw, int64_t batch,
-                double* sum_count, void* stream) {
+}  // extern "C"
+
+namespace {
+// {Σ logpdf, N} of this rank's shard, then the sum over the ranks; `flow`: θ raw
+// (normalised with the chain's bounds) or as given
+int nll(df_chain* chain, df_comm* comm, const float* x, const float* theta, int64_t batch, double* sum_count,
+        void* stream, bool flow) {
     if (!chain) return set_err(DF_ERR_INVALID, "null chain");
     if (!sum_count) return set_err(DF_ERR_INVALID, "null {Σ, count} output");
     if (comm && comm->device != chain->device)
         return set_err(DF_ERR_INVALID, "communicator and chain are bound to different devices");
-    int rc = df_flow_logpdf_sum(chain, x, theta_raw, sum_count, batch, stream);
+    int rc = flow ? df_flow_logpdf_sum(chain, x, theta, sum_count, batch, stream)
+                  : df_chain_logpdf_sum(chain, x, theta, sum_count, batch, stream);
     if (rc != DF_OK) return rc;
     DeviceGuard gd(chain->device);
     hipLaunchKernelGGL(set_count_kernel, dim3(1), dim3(1), 0, static_cast<hipStream_t>(stream), sum_count + 1,
@@ -199,6 +205,19 @@ int df_flow_nll(df_chain* chain, df_comm* comm, const float* x, const float* the
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_err(e, "count kernel launch");
     return comm ? df_comm_allreduce_sum(comm, sum_count, 2, DF_DTYPE_F64, stream) : DF_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int df_flow_nll(df_chain* chain, df_comm* comm, const float* x, const float* theta_raw, int64_t batch,
+                double* sum_count, void* stream) {
+    return nll(chain, comm, x, theta_raw, batch, sum_count, stream, true);
+}
+
+int df_chain_nll(df_chain* chain, df_comm* comm, const float* x, const float* theta, int64_t batch,
+                 double* sum_count, void* stream) {
+    return nll(chain, comm, x, theta, batch, sum_count, stream, false);
 }
 
 int df_train_allreduce_gradient(df_train* t, df_comm* comm, void* stream) {

@@ -115,8 +115,10 @@ int df_flow_sample(df_chain* c, float* x_out, const float* theta_raw, int theta_
         const int64_t need = (int64_t)n * batch;
         if (need > c->theta_ws_cap) {
             if (c->d_theta_ws) {
-                e = hipStreamSynchronize(st);  // an earlier launch may still read the old workspace
-                if (e != hipSuccess) return hip_err(e, "hipStreamSynchronize");
+                // the workspace belongs to the chain, not to a stream: an earlier sample on
+                // any stream may still read it
+                e = hipDeviceSynchronize();
+                if (e != hipSuccess) return hip_err(e, "hipDeviceSynchronize");
                 (void)hipFree(c->d_theta_ws);
             }
             c->d_theta_ws = nullptr;

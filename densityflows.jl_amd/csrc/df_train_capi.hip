@@ -71,6 +71,7 @@ struct TrainGraph {
     const void* theta = nullptr;
     const void* lp = nullptr;
     int64_t batch = 0, n_total = 0, cap_gen = -1, partial_gen = -1;
+    int flow = -1;                    // the θ convention it was recorded with (θ normalised in-kernel or not)
     int seen = 0;                     // eager runs with this key (captured on the second)
     hipGraphExec_t exec = nullptr;
     uint64_t last_use = 0;
@@ -106,6 +107,7 @@ struct df_train {
     float* d_ebuf = nullptr;
     double* d_lpsum = nullptr;
     bool debug = false;               // df_train_set_debug: refuse updates on a non-finite loss
+    int theta_input = DF_THETA_AUTO;  // df_train_set_theta_input
     const double* last_lp = nullptr;  // Σ logpdf written by the last df_train_gradient
     int64_t last_n = 0;               // ... and the n_total it was taken over
     int64_t cap = 0;       // batch capacity of snap / zbar / ebuf
@@ -970,6 +972,32 @@ int df_train_grad_ptr(df_train* t, float** grad_dev) {
     return DF_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Whether the kernels normalise θ for this trainer (df_theta_input); DF_THETA_RAW
+// without bounds on a conditional chain is an error (-1).
+int theta_flow(const df_train* t) {
+    const df_chain* c = t->c;
+    if (c->plan.n == 0) return 0;
+    switch (t->theta_input) {
+    case DF_THETA_GIVEN: return 0;
+    case DF_THETA_RAW: return c->has_bounds ? 1 : -1;
+    default: return c->has_bounds ? 1 : 0;
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int df_train_set_theta_input(df_train* t, int mode) {
+    if (!t) return set_err(DF_ERR_INVALID, "null trainer");
+    if (mode != DF_THETA_AUTO && mode != DF_THETA_RAW && mode != DF_THETA_GIVEN)
+        return set_err(DF_ERR_INVALID, "θ input mode must be DF_THETA_AUTO, DF_THETA_RAW or DF_THETA_GIVEN");
+    t->theta_input = mode;
+    return DF_OK;
+}
+
 int df_train_gradient(df_train* t, const float* x, const float* theta_raw, int64_t batch, int64_t n_total,
                       double* logpdf_sum, void* stream) {
     if (!t) return set_err(DF_ERR_INVALID, "null trainer");
@@ -990,9 +1018,11 @@ int df_train_gradient(df_train* t, const float* x, const float* theta_raw, int64
     if (!x) return set_err(DF_ERR_INVALID, "null input array");
     if (P.n > 0 && !theta_raw)
         return set_err(DF_ERR_SHAPE, "dimensions θ must match (n, dims...) with n number of trained parameters");
+    const int tf = theta_flow(t);
+    if (tf < 0) return set_err(DF_ERR_INVALID, "θ bounds not set (df_chain_set_theta_bounds) for DF_THETA_RAW");
+    const bool flow = tf == 1;
     int rc = ensure_capacity(t, batch);
     if (rc != DF_OK) return rc;
-    const bool flow = c->has_bounds && P.n > 0;
 
     // 1. inverse pass keeping every layer's output (U[li] = snap[li], U[0] = z)
     rc = run(c, MODE_LOGPDF, flow, x, theta_raw, nullptr, nullptr, nullptr, logpdf_sum ? logpdf_sum : t->d_lpsum,
@@ -1099,7 +1129,9 @@ int df_train_step_graph(df_train* t, const float* x, const float* theta_raw, int
         int rc = df_train_gradient(t, x, theta_raw, batch, n_total, logpdf_sum, stream);
         return rc != DF_OK ? rc : df_train_apply(t, stream);
     }
-    if (g && (g->cap_gen != t->cap_gen || g->partial_gen != t->c->partial_gen)) {  // stale buffers
+    const int flow_now = theta_flow(t);
+    if (g && (g->cap_gen != t->cap_gen || g->partial_gen != t->c->partial_gen ||
+              g->flow != flow_now)) {  // stale buffers, or θ now read the other way
         if (g->exec) (void)hipGraphExecDestroy(g->exec);
         g->exec = nullptr;
         g->seen = 0;
@@ -1130,6 +1162,7 @@ int df_train_step_graph(df_train* t, const float* x, const float* theta_raw, int
         int rc = df_train_gradient(t, x, theta_raw, batch, n_total, logpdf_sum, stream);
         if (rc == DF_OK) rc = df_train_apply(t, stream);
         g->seen = 1;
+        g->flow = flow_now;
         g->cap_gen = t->cap_gen;
         g->partial_gen = t->c->partial_gen;
         g->last_use = now;

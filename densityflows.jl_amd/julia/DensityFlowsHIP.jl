@@ -13,12 +13,28 @@ so `Flow`'s @flow_wrapper methods (src/Macros.jl:104-112), `logpdf`
 (src/Flows.jl:272-281) and `sample` (src/Flows.jl:157-192) run on the MI355X
 unchanged once the chain is wrapped: `FlowChain((HIPFlowChain(chain),))`.
 
-STATUS: written against include/densityflows_hip.h (ABI 3; `__init__` refuses a
+STATUS: written against include/densityflows_hip.h (ABI 4; `__init__` refuses a
 library of another ABI) but NOT executed — there is no Julia toolchain in this
-build pipeline (SURVEY.md §8c).  The same entry points are exercised from
-Python (densityflows.jl_amd/_lib.py) by the parity tests, and
-tests/test_julia_shim.py checks this file's method signatures statically
-against the reference's (dispatch specificity, AbstractArray inputs).
+build pipeline (SURVEY.md §8c).  Not executed in particular: the Functors walk
+that `Optimisers.setup(Adam(η), flow.model)` makes over HIPFlowChain (declared
+below with `@functor HIPFlowChain (params,)`), `hip_flow` / `load_flow` and
+`copy_trainables!`.  What IS executed on the GPU: tests/julia_replay.py replays,
+ccall for ccall, the C-call sequence of this file's HIPFlowChain, forward /
+backward, logpdf_sum, HIPTrainer, train_step!, _hip_train!, _set_bounds! and
+_hip_sample (tests/test_gpu_julia_replay.py, against the oracle's epoch loop),
+and tests/test_julia_shim.py checks statically that the replay issues the
+same ccall symbols in the same order as each of those functions here, that
+every ccall matches the header, and the method signatures against the
+reference's (dispatch specificity, AbstractArray inputs).
+
+θ CONTRACT.  Model-level calls take θ as given, as the reference's model
+methods do (train! normalises once, src/Flows.jl:391-392): forward / backward /
+forward! (df_chain_*), logpdf_sum (df_chain_logpdf_sum), flow_nll
+(df_chain_nll) and every HIPTrainer step (created with DF_THETA_GIVEN, so
+the chain's θ bounds never reach them).  Flow-level calls take raw θ and
+normalise it in the kernel with the Flow's MetaData bounds: only `sample`
+(df_flow_sample after _set_bounds!), matching @flow_wrapper
+(src/Macros.jl:104-112).
 
 Host `Array{Float32}` arguments are staged through device buffers
 (df_device_alloc / df_memcpy_*); device arrays (AMDGPU.jl `ROCArray`) can be
@@ -36,7 +52,7 @@ export HIPFlowChain, HIPTrainer, HIPComm, train_step!, train_step_graph!, train_
        copy_trainables!, hip_flow, flow_nll, sample
 
 const LIB = get(ENV, "DENSITYFLOWS_HIP_LIB", joinpath(@__DIR__, "..", "libdensityflows_hip.so"))
-const ABI_VERSION = Int32(3)
+const ABI_VERSION = Int32(4)
 
 function __init__()
     v = ccall((:df_get_abi_version, LIB), Cint, ())
@@ -122,7 +138,10 @@ mutable struct HIPFlowChain <: FlowElement
     bounds::Any                     # θ bounds last given to df_chain_set_theta_bounds
 end
 
-# Optimisers.setup(rule, FlowChain((HIPFlowChain(chain),))) yields a Leaf holding `rule`
+# Optimisers.setup(rule, FlowChain((HIPFlowChain(chain),))) yields a Leaf holding `rule`:
+# the chain is a functor whose only child is the flat parameter vector (the handle,
+# staging buffers and trainer are not walked), and that child is its trainable
+Optimisers.Functors.@functor HIPFlowChain (params,)
 Optimisers.trainable(c::HIPFlowChain) = (; params = c.params)
 
 # flatten the chain into (element index, layer) pairs; blocks share an element
@@ -250,14 +269,16 @@ function forward!(c::HIPFlowChain, z::AbstractArray{Float32,N}, θ::AbstractArra
 end
 
 """Σ_j logpdf_j (fp64, on the device) of the chain's inverse pass under MvNormal(0, I):
-the sum src/Flows.jl:352-359 averages.  θ as given (already normalised)."""
+the sum src/Flows.jl:352-359 averages.  θ as given (already normalised, as
+normalized_training_data returns it): df_chain_logpdf_sum, whatever bounds the
+chain holds."""
 function logpdf_sum(c::HIPFlowChain, x::AbstractArray{Float32,N}, θ::AbstractArray{Float32,N}) where {N}
     x, θ = _dense(x), _dense(θ)
     B = prod(size(x)[2:N])
     dx, dθ, ds = _buf!(c.stage, 1, sizeof(x)), _buf!(c.stage, 2, sizeof(θ)), _buf!(c.stage, 5, 16)
     _h2d(dx, x); c.n > 0 && _h2d(dθ, θ)
-    check(ccall((:df_flow_logpdf_sum, LIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
-                c.handle, dx, c.n > 0 ? dθ : C_NULL, ds, B, C_NULL), "df_flow_logpdf_sum")
+    check(ccall((:df_chain_logpdf_sum, LIB), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
+                c.handle, dx, c.n > 0 ? dθ : C_NULL, ds, B, C_NULL), "df_chain_logpdf_sum")
     r = Vector{Float64}(undef, 1)
     _d2h(r, ds)
     return r[1]
@@ -286,20 +307,23 @@ function _destroy!(t::HIPTrainer)
     return nothing
 end
 
-"""Optimisers.setup(Adam(η, β, ϵ), model) on the device; the trainer owns the flat trainables."""
+"""Optimisers.setup(Adam(η, β, ϵ), model) on the device; the trainer owns the flat trainables.
+Its steps take θ as given (DF_THETA_GIVEN: normalised, as train! passes it to the model)."""
 function HIPTrainer(c::HIPFlowChain; eta=1f-3, beta=(0.9f0, 0.999f0), epsilon=1f-8)
     t = Ref{Ptr{Cvoid}}(C_NULL)
     check(ccall((:df_train_create, LIB), Cint, (Ptr{Ptr{Cvoid}}, Ptr{Cvoid}, Ref{AdamDesc}),
                 t, c.handle, AdamDesc(eta, beta[1], beta[2], epsilon)), "df_train_create")
     n = Ref{Int64}(0)
     check(ccall((:df_train_num_params, LIB), Cint, (Ptr{Cvoid}, Ref{Int64}), t[], n), "df_train_num_params")
+    check(ccall((:df_train_set_theta_input, LIB), Cint, (Ptr{Cvoid}, Cint), t[], DF_THETA_GIVEN),
+          "df_train_set_theta_input")
     obj = HIPTrainer(t[], c, n[], Staging(3))
     finalizer(_destroy!, obj)
     return obj
 end
 
-"""One mini-batch step of train! (gradient of loss(backward(m, x, θ)) + Adam update).
-Returns the batch loss before the update (−Σ logpdf / B)."""
+"""One mini-batch step of train! (gradient of loss(backward(m, x, θ)) + Adam update),
+θ as given (normalised).  Returns the batch loss before the update (−Σ logpdf / B)."""
 function train_step!(t::HIPTrainer, x::AbstractArray{Float32,N}, θ::AbstractArray{Float32,N}) where {N}
     x, θ = _dense(x), _dense(θ)
     B = prod(size(x)[2:N])
@@ -316,6 +340,7 @@ function train_step!(t::HIPTrainer, x::AbstractArray{Float32,N}, θ::AbstractArr
 end
 
 const DF_ERR_NONFINITE = Cint(-6)
+const DF_THETA_GIVEN = Cint(2)      # df_theta_input
 
 """The debug check of df_train_step refused an update (NaN / Inf loss)."""
 struct NonFiniteLoss <: Exception
@@ -325,7 +350,7 @@ end
 """
     train_step_graph!(t, x_dev, θ_dev, B)
 
-train_step! on device buffers that stay the same across the mini-batch loop
+train_step! (θ as given) on device buffers that stay the same across the mini-batch loop
 (copy each batch into them): the step is captured as one hipGraph the second
 time the buffers repeat and replayed afterwards (df_train_step_graph).
 """
@@ -386,8 +411,9 @@ end
     flow_nll(c::HIPFlowChain, comm, x_shard, θ_shard) -> loss
 
 Config 3's sharded NLL, `loss = -mean(logpdf)` (src/Flows.jl:352-359) over the
-union of every rank's shard: df_flow_nll all-reduces {Σ logpdf, N} over RCCL.
-θ as given (already normalised).  `comm = nothing`: this process only.
+union of every rank's shard: df_chain_nll all-reduces {Σ logpdf, N} over RCCL.
+θ as given (already normalised, as train!'s epoch losses take it); the chain's
+bounds are not consulted.  `comm = nothing`: this process only.
 """
 function flow_nll(c::HIPFlowChain, comm::Union{HIPComm,Nothing}, x::AbstractArray{Float32,N},
                   θ::AbstractArray{Float32,N}) where {N}
@@ -395,10 +421,10 @@ function flow_nll(c::HIPFlowChain, comm::Union{HIPComm,Nothing}, x::AbstractArra
     B = prod(size(x)[2:N])
     dx, dθ, ds = _buf!(c.stage, 1, sizeof(x)), _buf!(c.stage, 2, sizeof(θ)), _buf!(c.stage, 5, 16)
     _h2d(dx, x); c.n > 0 && _h2d(dθ, θ)
-    check(ccall((:df_flow_nll, LIB), Cint,
+    check(ccall((:df_chain_nll, LIB), Cint,
                 (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Ptr{Cvoid}),
                 c.handle, comm === nothing ? C_NULL : comm.handle, dx, c.n > 0 ? dθ : C_NULL, B, ds, C_NULL),
-          "df_flow_nll")
+          "df_chain_nll")
     r = Vector{Float64}(undef, 2)
     _d2h(r, ds)
     return Float32(-r[1] / r[2])
@@ -407,8 +433,8 @@ end
 """
     train_step_dist!(t, comm, x_shard, θ_shard, n_total)
 
-One data-parallel train! step: this rank's gradient with the mean over the global
-batch `n_total`, RCCL all-reduce of ∇ and Σ logpdf, the identical Adam step on
+One data-parallel train! step (θ as given, normalised): this rank's gradient with
+the mean over the global batch `n_total`, RCCL all-reduce of ∇ and Σ logpdf, the identical Adam step on
 every rank (df_train_step_dist).  Returns the global batch loss before the update.
 """
 function train_step_dist!(t::HIPTrainer, comm::HIPComm, x::AbstractArray{Float32,N}, θ::AbstractArray{Float32,N},

@@ -110,6 +110,11 @@ class HIPTrainer:
         (df_train_set_debug → NonFiniteError)."""
         _lib.check(self.lib.df_train_set_debug(self.handle, 1 if on else 0))
 
+    def set_theta_input(self, mode: int) -> None:
+        """df_train_set_theta_input: _lib.DF_THETA_AUTO (default; normalise θ iff the
+        chain has bounds), DF_THETA_RAW (always normalise) or DF_THETA_GIVEN (never)."""
+        _lib.check(self.lib.df_train_set_theta_input(self.handle, int(mode)), "df_train_set_theta_input")
+
     def allreduce_gradient(self, comm) -> None:
         """Sum the flat gradient over the ranks of ``comm`` (df_train_allreduce_gradient)."""
         _lib.check(self.lib.df_train_allreduce_gradient(self.handle, comm.handle, _stream(self.device)),

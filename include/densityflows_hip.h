@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DF_ABI_VERSION 3
+#define DF_ABI_VERSION 4
 
 typedef enum df_status {
     DF_OK = 0,
@@ -179,6 +179,16 @@ int df_chain_backward(df_chain* chain, const float* x, const float* theta,
 int df_chain_forward_inplace(df_chain* chain, float* z, const float* theta,
                              int64_t batch, void* stream);
 
+/* df_chain_logpdf / df_chain_logpdf_sum: the same quantities as df_flow_logpdf /
+ * df_flow_logpdf_sum below with θ used as given — logpdf / loss of the MODEL,
+ * as train! evaluates them on normalized_training_data (src/Flows.jl:391-392,
+ * 419-430): backward(flow.model, x, t) then the MvNormal(0, I) log-density.
+ * Independent of the chain's θ bounds. */
+int df_chain_logpdf(df_chain* chain, const float* x, const float* theta,
+                    float* logpdf_out, int64_t batch, void* stream);
+int df_chain_logpdf_sum(df_chain* chain, const float* x, const float* theta,
+                        double* sum_out, int64_t batch, void* stream);
+
 /* ---- flow level (θ raw, normalised in-kernel with the stored bounds) -----
  * The @flow_wrapper methods (src/Macros.jl:104-112, applied at
  * src/DensityFlows.jl:72): f(flow, y, θ) = f(flow.model, y, normalize_input(θ)).
@@ -250,11 +260,31 @@ int df_train_create(df_train** out, df_chain* chain, const df_adam* opt);
 int df_train_destroy(df_train* t);
 /* Number of trainable parameters (length of the flat vectors below). */
 int df_train_num_params(const df_train* t, int64_t* count);
+/* How the trainer's entry points (df_train_gradient and every step built on
+ * it) read θ.  train! feeds the model normalised θ (normalized_training_data,
+ * src/Data.jl:189-193, src/Flows.jl:391-392); a host may instead hand over the
+ * raw θ and let the kernels normalise it with the Flow's MetaData bounds.
+ *   DF_THETA_AUTO  (the default): normalise iff the chain has θ bounds
+ *                  (df_chain_set_theta_bounds) at the time of the call;
+ *   DF_THETA_RAW:  θ is raw and always normalised with the chain's bounds
+ *                  (n > 0 without bounds: DF_ERR_INVALID);
+ *   DF_THETA_GIVEN: θ is used as given (already normalised); the chain's
+ *                  bounds are never consulted, so a later
+ *                  df_chain_set_theta_bounds (e.g. by sample) cannot change
+ *                  what this trainer computes.
+ * A captured df_train_step_graph step is re-captured when the effective
+ * convention changes. */
+typedef enum df_theta_input {
+    DF_THETA_AUTO = 0,
+    DF_THETA_RAW = 1,
+    DF_THETA_GIVEN = 2
+} df_theta_input;
+int df_train_set_theta_input(df_train* t, int mode);
 /* Gradient of loss over this batch with the mean taken over `n_total`
  * samples (n_total = batch on one GPU; the global batch under data
- * parallelism, so the per-rank gradients SUM to the global one).  θ is
- * normalised with the chain's bounds when set (df_chain_set_theta_bounds),
- * as train! does with normalized_training_data (src/Data.jl:189-193).
+ * parallelism, so the per-rank gradients SUM to the global one).  θ as the
+ * trainer's df_theta_input says (default: normalised with the chain's
+ * bounds when set).
  * The result is left in the device buffer returned by df_train_grad_ptr.
  * `logpdf_sum` (device double, may be NULL) receives Σ logpdf of the batch
  * at the current parameters (the loss before the update is -Σ/n_total). */
@@ -322,6 +352,10 @@ int df_comm_allreduce_sum(df_comm* comm, void* buf_dev, int64_t count, int dtype
  * holds the global {Σ, N}; loss = -Σ / N.  comm = NULL: this process only. */
 int df_flow_nll(df_chain* chain, df_comm* comm, const float* x, const float* theta_raw, int64_t batch,
                 double* sum_count, void* stream);
+/* df_flow_nll with θ used as given (normalised): the sharded loss of the model
+ * on normalized data, as train!'s epoch losses (src/Flows.jl:419-430). */
+int df_chain_nll(df_chain* chain, df_comm* comm, const float* x, const float* theta, int64_t batch,
+                 double* sum_count, void* stream);
 /* All-reduce (sum) of the flat gradient of df_train_gradient; every rank must
  * have called df_train_gradient with n_total = the global batch. */
 int df_train_allreduce_gradient(df_train* t, df_comm* comm, void* stream);

@@ -53,3 +53,20 @@ def test_train_split_flops_pricing():
     cfg4 = bench.build_chain("cfg4")
     per_net = 2 * (24 * 256 + 256 * 256 + 256 * 16) + 2 * 2 * 256 * 256
     assert bench.train_split_flops(cfg4, 6) == 32 * per_net
+
+
+def test_gpus8_dry_run_reports_every_rank():
+    """the 1→8 run is self-diagnosing — 8 ranks launched by
+    bench.py itself (gloo on CPU), rank 0 reports n_gpus 8 and the per-rank
+    timing spread gathered from all 8."""
+    r = _run(["--gpus", "8", "--steps", "2", "--warmup", "1", "--dry-run"], {"DF_DIST_BACKEND": "gloo"},
+             timeout=400)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["dry_run"] is True
+    ranks = out["ranks"]
+    assert ranks["n"] == 8 and ranks["group_size"] == 8 and len(ranks["kernel_ms_per_rank"]) == 8
+    assert ranks["wall_ms_per_step_min"] <= ranks["wall_ms_per_step_max"]
+    assert ranks["process_group"] == "torch.distributed gloo"

@@ -19,7 +19,11 @@ PROBE = os.path.join(ROOT, "tools", "probe", "dot2_split")
 @pytest.mark.gpu
 def test_split_helper_planes_bitwise():
     if not os.path.exists(PROBE):
-        pytest.skip("tools/probe/dot2_split was not built (__graft_entry__.build(): make probe)")
+        # the only bitwise evidence for split8_mrem (the SPLIT kernel's default): a missing
+        # probe fails the GPU suite unless the run opts out explicitly
+        if os.environ.get("DF_ALLOW_NO_PROBE") == "1":
+            pytest.skip("tools/probe/dot2_split was not built and DF_ALLOW_NO_PROBE=1")
+        pytest.fail("tools/probe/dot2_split was not built (__graft_entry__.build(): make probe)")
     r = subprocess.run([PROBE], capture_output=True, text=True, timeout=60)
     print(r.stdout)
     lines = [l for l in r.stdout.splitlines() if l.startswith(("split2 helper", "vgpr-const", "split8 mrem"))]

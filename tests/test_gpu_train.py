@@ -649,3 +649,37 @@ def test_train_epochs_match_oracle_loop(cuda):
     print("train_loss", flow.train_loss, tl, "valid_loss", flow.valid_loss, vl)
     np.testing.assert_allclose(flow.train_loss, tl, rtol=2e-4)
     np.testing.assert_allclose(flow.valid_loss, vl, rtol=2e-4)
+
+
+def test_graph_step_survives_clock_probe_toggle_and_growth(cuda):
+    """the clock-stamp buffer is an eager-launch diagnostic.
+    A graph step captured with the probe off, then the probe switched on, the stamp
+    buffer grown by a larger eager pass and the graph replayed: the replays match an
+    eager twin bitwise, and a capture with the probe on records no stamps (nothing
+    is allocated inside the capture)."""
+    import torch
+
+    spec, chain, d, n = _setup("readme")
+    x, th = _inputs(d, n, 512, seed=21)
+    a = HIPTrainer(spec_to_element(spec).hip(), Adam())
+    b = HIPTrainer(spec_to_element(spec).hip(), Adam())
+    xb, tb = _dev(x, cuda), _dev(th, cuda)
+    for _ in range(3):                                   # eager, capture, replay (probe off)
+        a.step_graph(xb, tb, 512)
+        b.step(xb, tb, 512)
+    a.chain.clock_probe(True)
+    xl, tl = _inputs(d, n, 1 << 18, seed=22)
+    a.chain.apply("backward", xl, tl)                     # eager pass: grows the stamp slots
+    torch.cuda.synchronize()
+    assert a.chain.clock_read()[2] > 0
+    for _ in range(3):                                   # replays of the probe-off capture
+        a.step_graph(xb, tb, 512)
+        b.step(xb, tb, 512)
+    x2, th2 = _inputs(d, n, 300, seed=23)                # a new key captured with the probe on
+    xb2, tb2 = _dev(x2, cuda), _dev(th2, cuda)
+    for _ in range(3):
+        a.step_graph(xb2, tb2, 300)
+        b.step(xb2, tb2, 300)
+    a.chain.clock_probe(False)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(a.get_params(), b.get_params())

@@ -250,7 +250,7 @@ def test_julia_shim_binds_only_declared_symbols():
     called = set(re.findall(r"ccall\(\(:?\(?:?(df_[a-z0-9_]+)", src)) | set(re.findall(r":(df_[a-z0-9_]+)", src))
     assert called, "no ccall found"
     assert called <= declared, sorted(called - declared)
-    for sym in ("df_chain_forward_inplace", "df_flow_logpdf_sum", "df_flow_nll", "df_train_step",
+    for sym in ("df_chain_forward_inplace", "df_chain_logpdf_sum", "df_chain_nll", "df_train_step",
                 "df_train_step_dist", "df_train_set_debug", "df_comm_init_rank", "df_comm_get_unique_id"):
         assert sym in called, sym
     # block balance: every opener (function/struct/if/for/try/begin/do/let/module) has an `end`

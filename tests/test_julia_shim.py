@@ -113,3 +113,74 @@ def test_sample_methods_narrow_the_flow_only(shim):
     assert re.search(r"sample\(rng::Random\.AbstractRNG, flow::Flow\{T,D,N,<:HIPModel\}, "
                      r"dims::Tuple\{Vararg\{Integer\}\},\s*θ::NTuple\{N,T\}\)", shim)
     assert ":df_flow_sample" in shim
+
+
+def _julia_ccalls_by_function(text):
+    """Julia function name -> literal ccall symbols of its methods, in source order."""
+    text = re.sub(r'"""(.*?)"""', lambda m: "\n" * m.group(0).count("\n"), text, flags=re.S)
+    lines = text.split("\n")
+    out, i = {}, 0
+    while i < len(lines):
+        ln = lines[i]
+        m = re.match(r"function ([\w!]+)\(", ln)
+        if m:
+            j = i + 1
+            while lines[j] != "end":
+                j += 1
+        else:
+            m = re.match(r"([A-Za-z_][\w!]*)\(", ln)
+            if not m:
+                i += 1
+                continue
+            j = i + 1
+            while j < len(lines) and lines[j][:1] in (" ", "\t"):
+                j += 1
+            j -= 1
+        body = "\n".join(lines[i:j + 1])
+        out.setdefault(m.group(1), []).extend(re.findall(r"ccall\(\(:(\w+), LIB\)", body))
+        i = j + 1
+    return {k: v for k, v in out.items() if v}
+
+
+def _replay_ccalls_by_function():
+    import ast
+
+    path = os.path.join(ROOT, "tests", "julia_replay.py")
+    with open(path) as f:
+        tree = ast.parse(f.read())
+    out = {}
+    for node in tree.body:
+        if not isinstance(node, ast.FunctionDef):
+            continue
+        calls = [c for c in ast.walk(node) if isinstance(c, ast.Call) and isinstance(c.func, ast.Name)
+                 and c.func.id == "cc" and c.args and isinstance(c.args[0], ast.Constant)]
+        calls.sort(key=lambda c: (c.lineno, c.col_offset))
+        if calls:
+            out[node.name] = [c.args[0].value for c in calls]
+    return out
+
+
+def test_replay_issues_the_shims_ccalls(shim):
+    """tests/julia_replay.py (run on the GPU by test_gpu_julia_replay.py) re-enacts
+    each shim function: the same literal ccall symbols in the same order."""
+    jl = _julia_ccalls_by_function(shim)
+    py = _replay_ccalls_by_function()
+    assert len(jl) >= 20, sorted(jl)
+    for name, syms in jl.items():
+        pyname = name.replace("!", "_bang")
+        assert pyname in py, f"{name} has no replay in tests/julia_replay.py"
+        assert py[pyname] == syms, f"{name}: shim {syms}, replay {py[pyname]}"
+    assert set(py) <= {n.replace("!", "_bang") for n in jl}, sorted(set(py) - {n.replace("!", "_bang") for n in jl})
+
+
+def test_model_level_calls_take_theta_as_given(shim):
+    """The θ contract: model-level entry points never read the
+    chain's θ bounds — only sample goes through a df_flow_* entry point."""
+    jl = _julia_ccalls_by_function(shim)
+    for name in ("logpdf_sum", "flow_nll", "train_step!", "train_step_dist!", "train_step_graph!"):
+        assert not any(s.startswith("df_flow_") for s in jl[name]), (name, jl[name])
+    assert jl["HIPTrainer"][-1] == "df_train_set_theta_input"
+    assert re.search(r"df_train_set_theta_input, LIB\), Cint, \(Ptr\{Cvoid\}, Cint\), t\[\], DF_THETA_GIVEN\)", shim)
+    assert re.search(r"const DF_THETA_GIVEN = Cint\(2\)", shim)
+    flow_syms = {s for v in jl.values() for s in v if s.startswith("df_flow_")}
+    assert flow_syms == {"df_flow_sample"}, flow_syms
