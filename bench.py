@@ -464,7 +464,7 @@ def main():
     if clock is not None and args.mode != "train":
         # clock-normalised time: shader cycles per launch of the clock run (comparable across
         # boxes and DVFS states)
-        clock["kernel_mcycles_per_launch"] = round(clock["clock_run_ms_per_step"] * clock["ghz_median"] * 1e3, 4)
+        clock["kernel_mcycles_per_launch"] = round(clock["clock_run_ms_per_step"] * clock["ghz_median"], 4)
     flop = info.flops_per_sample * B
     achieved_tflops = flop / kernel_s / 1e12
     hbm_algo = (8.0 * d + 4.0 * n + 4.0) * B          # read z (+θ), write x, ldj

@@ -53,6 +53,60 @@ bool use_split(const df_chain* c) { return c->plan.split && !c->exact; }
 
 bool use_wsplit(const df_chain* c) { return c->plan.wsplit && !c->exact; }
 
+// The descriptor of the small-batch kernel (df_kernels.h SmallDesc) for this launch.
+static df::SmallDesc small_desc(const df_chain* c, bool flow) {
+    const df::Plan& P = c->plan;
+    df::SmallDesc sd{};
+    for (int li = 0; li < P.n_layers && li < df::kSmallLayers; ++li) {
+        const df::ULayer& U = P.ulayers[li];
+        sd.kind[li] = (int8_t)U.kind;
+        sd.elem_start[li] = (int8_t)U.elem_start;
+        sd.elem_end[li] = (int8_t)U.elem_end;
+        sd.alpha[li] = U.alpha;
+        sd.beta[li] = U.beta;
+        sd.ldj_const[li] = U.ldj_const;
+        if (U.kind == DF_LAYER_NORM) {
+            for (int i = 0; i < P.d && i < 8; ++i) {
+                sd.xmin[li][i] = P.params[U.norm_off + i];
+                sd.xmax[li][i] = P.params[U.norm_off + P.d + i];
+            }
+            continue;
+        }
+        sd.n_out[li] = (int8_t)U.t.n_out;
+        for (int k = 0; k < 4; ++k) {
+            sd.feat[li][k] = (int8_t)P.tables[U.feat_tab + k];
+            sd.af[li][k] = (int8_t)(k < U.n_af ? P.tables[U.af_tab + k] : 0);
+        }
+        const df::UNet* nets[2] = {&U.s, &U.t};
+        for (int k = 0; k < 2; ++k) {
+            if (k == 0 && U.kind != DF_LAYER_RNVP) continue;
+            const int64_t base = P.stages[nets[k]->stage].src_off;
+            sd.w0[li][k] = (int32_t)(base + nets[k]->off_w0);
+            sd.wh[li][k] = (int32_t)(base + nets[k]->off_h);
+            sd.wo[li][k] = (int32_t)(base + nets[k]->off_out);
+        }
+    }
+    sd.norm_theta = (flow && P.n > 0) ? 1 : 0;
+    for (int i = 0; sd.norm_theta && i < P.n && i < 8; ++i) {
+        sd.tmin[i] = c->h_bounds[i];
+        sd.tmax[i] = c->h_bounds[P.n + i];
+    }
+    return sd;
+}
+
+// The small-batch kernel (df_small.hip) for a batch that underfills the chip: FAST
+// exact-f32 chains (relu _dflt_net, one hidden Dense, folded first-Dense bias, <= 4
+// outputs) of hidden 16 with n + d <= 8 and at most 4 layers (the README chain of
+// config 1).  DF_SMALL_MAX (samples) moves the crossover; 0 disables it.
+static bool use_small(const df_chain* c, int64_t batch) {
+    const df::Plan& P = c->plan;
+    if (!(P.uniform && P.fast && P.outv && P.ht == 1 && P.n + P.d <= 8 && P.n_layers <= df::kSmallLayers))
+        return false;
+    int64_t max_b = (int64_t)df::kSmallSamples * 8 * c->n_cu;
+    if (const char* e = std::getenv("DF_SMALL_MAX")) max_b = std::atoll(e);
+    return batch <= max_b;
+}
+
 static size_t lds_for_tiles(const df_chain* c, int t, bool split = false) {
     const df::Plan& P = c->plan;
     if (split)
@@ -208,7 +262,7 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
     // the fp64 workgroup reduction of the logpdf epilogue (>= 64 B).
     c->stage_bytes = P.stage_max < 1024 ? 1024 : P.stage_max;
     c->n_stage_bufs = P.stages.size() > 1 ? 2 : 1;
-    c->tab_bytes = ((int)P.tables.size() * 4 + 15) / 16 * 16;
+    c->tab_bytes = df::table_lds_bytes(P);
     c->lds = (size_t)c->stage_bytes * c->n_stage_bufs + c->tab_bytes +
              (size_t)P.samples_per_block * P.stride * 4;
     if (c->lds > 160 * 1024) {
@@ -373,6 +427,7 @@ int df_chain_set_theta_bounds(df_chain* c, const float* tmin, const float* tmax)
     DeviceGuard gd(c->device);
     hipError_t e = hipMemcpy(c->d_bounds, b.data(), sizeof(float) * 2 * n, hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_err(e, "hipMemcpy(θ bounds)");
+    c->h_bounds = b;
     c->has_bounds = true;
     return DF_OK;
 }
@@ -405,19 +460,21 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
     const bool wide = P.wide && !(std::getenv("DF_NO_WIDE") && std::getenv("DF_NO_WIDE")[0] == '1');
     const bool split = !wide && use_split(c);
-    const int tiles = wide ? df::kWideT : choose_tiles(c, mode, batch, split);
+    const bool small = !wide && !split && use_small(c, batch);
+    const int tiles = wide ? df::kWideT : small ? 2 : choose_tiles(c, mode, batch, split);
     if (const char* dbg = std::getenv("DF_DEBUG_LAUNCH")) {  // tuning aid: the launch shape on stderr
         if (dbg[0] == '1') {
             std::fprintf(stderr, "[df] mode %d batch %lld kernel %s tiles %d (max %d) occupancy:", mode,
                          (long long)batch,
-                         wide ? (use_wsplit(c) ? "wide-split" : "wide") : !P.uniform ? "generic" : split ? "uniform-fast-split" : P.fast ? "uniform-fast" : "uniform",
+                         wide ? (use_wsplit(c) ? "wide-split" : "wide") : small ? "small" : !P.uniform ? "generic" : split ? "uniform-fast-split" : P.fast ? "uniform-fast" : "uniform",
                          tiles, split ? P.stiles : P.tiles);
             for (int t = 1; t <= (split ? P.stiles : P.tiles); ++t)
                 std::fprintf(stderr, " t%d=%d", t, split ? c->socc[mode][t] : c->occ[mode][t]);
             std::fprintf(stderr, "\n");
         }
     }
-    const int64_t S = wide ? (int64_t)df::kWideWaves * 16 * df::kWideT : (int64_t)df::kWavesPerBlock * 16 * tiles;
+    const int64_t S = wide ? (int64_t)df::kWideWaves * 16 * df::kWideT
+                           : small ? (int64_t)df::kSmallSamples : (int64_t)df::kWavesPerBlock * 16 * tiles;
     const int64_t grid = (batch + S - 1) / S;
     if (grid > 0x7fffffff) return set_err(DF_ERR_UNSUPPORTED, "batch too large for one launch");
     if (sum_out && grid > c->partial_cap) {
@@ -472,6 +529,7 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     a.n_layers = P.n_layers;
     a.tab_ints = (int)P.tables.size();
     a.tab_bytes = c->tab_bytes;
+    a.n_par = (int)P.params.size();
     a.stage_bytes = c->stage_bytes;
     a.n_stage_bufs = c->n_stage_bufs;
     a.sched_fwd = static_cast<const int32_t*>(c->d_sched);
@@ -511,6 +569,8 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
         } else {
             e = df::launch_wide(mode, a, (unsigned)grid, c->wide_lds, st);
         }
+    } else if (small) {
+        e = df::launch_small(mode, a, small_desc(c, flow), (unsigned)grid, st);
     } else if (split) {
         a.blob = static_cast<const uint8_t*>(c->d_sblob);
         a.stages = static_cast<const df::DevStage*>(c->d_sstages);

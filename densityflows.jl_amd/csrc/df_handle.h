@@ -25,6 +25,7 @@ struct df_chain {
     void* d_params = nullptr;
     float* d_bounds = nullptr;  // [θmin (n) | θmax (n)]
     bool has_bounds = false;
+    std::vector<float> h_bounds;  // host copy of d_bounds (the small-batch kernel's descriptor)
     double* d_partial = nullptr;
     int64_t partial_cap = 0;
     int64_t partial_gen = 0;  // bumped when d_partial is reallocated (captured train graphs hold it)

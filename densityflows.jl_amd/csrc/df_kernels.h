@@ -35,7 +35,8 @@ struct ChainArgs {
     int d, n, stride, n_layers;
     int tiles;           // 16-sample tiles per wave resident in LDS (Plan::tiles)
     int tab_ints;
-    int tab_bytes;       // LDS bytes reserved for tables (16-B multiple)
+    int tab_bytes;       // LDS bytes reserved for tables (16-B multiple; specialised kernel: + n_par bounds)
+    int n_par;           // specialised kernel: floats of `params` copied to LDS after the tables
     int stage_bytes;     // LDS bytes of ONE stage buffer (multiple of 1 KiB)
     int n_stage_bufs;    // 1 (single-stage chain) or 2 (double-buffered)
     const int32_t* sched_fwd;
@@ -103,5 +104,25 @@ hipError_t launch_reduce_partials(const double* part, int64_t n, double* out, hi
 // split: the SPLIT variant (bf16x3 products; a.blob / stages / schedules / wlayers / tables are the split ones)
 hipError_t launch_wide(int mode, const ChainArgs& a, unsigned grid, size_t lds, hipStream_t st, bool split = false);
 hipError_t set_wide_lds_limit(size_t lds, bool split = false);
+
+// Small-batch kernel (df_small.hip): FAST exact-f32 chains of hidden 16 with n + d <= 8 and
+// at most kSmallLayers layers; one wave of 16 samples per workgroup.
+constexpr int kSmallSamples = 16;
+constexpr int kSmallLayers = 4;
+// Everything the small-batch kernel reads besides the blob and the batch arrays, passed
+// BY VALUE as a kernel argument: it arrives with the kernel arguments, so the weight
+// loads need no dependent scalar-memory round trips (descriptor → stage → fragments)
+// before they can issue.  Built on the host from the plan (df_capi.hip small_desc).
+struct SmallDesc {
+    int32_t w0[kSmallLayers][2], wh[kSmallLayers][2], wo[kSmallLayers][2];  // blob byte offsets, net s / t
+    int8_t kind[kSmallLayers], elem_start[kSmallLayers], elem_end[kSmallLayers], n_out[kSmallLayers];
+    int8_t feat[kSmallLayers][4];  // state columns of the conditioner features k = lane group
+    int8_t af[kSmallLayers][4];    // state columns of the transformed dims
+    float alpha[kSmallLayers], beta[kSmallLayers], ldj_const[kSmallLayers];
+    float xmin[kSmallLayers][8], xmax[kSmallLayers][8];  // NormalizationLayer bounds (d <= 8)
+    float tmin[8], tmax[8];                              // θ bounds (n <= 8)
+    int32_t norm_theta;                                  // θ raw: normalise it with tmin / tmax
+};
+hipError_t launch_small(int mode, const ChainArgs& a, const SmallDesc& sd, unsigned grid, hipStream_t st);
 
 }  // namespace df

@@ -269,7 +269,7 @@ void build_split(const df_chain_desc* desc, Plan& P, const std::vector<char>& fo
     int target = kLdsPerBlockTarget;
     if (const char* e = std::getenv("DF_SPLIT_LDS_KB")) target = std::max(32, std::atoi(e)) * 1024;
     const int nbuf = P.sstages.size() > 1 ? 2 : 1;
-    const int fixed = nbuf * P.sstage_max + round_up((int)P.tables.size() * 4, 16);
+    const int fixed = nbuf * P.sstage_max + table_lds_bytes(P);
     const int per_tile = kWavesPerBlock * 16 * P.stride * 4;
     int t = 0;
     while (t < kMaxTilesPerWave && fixed + (t + 1) * per_tile <= target) ++t;
@@ -528,7 +528,7 @@ void build_wide_split(const df_chain_desc* desc, Plan& P) {
 }  // namespace
 
 size_t plan_lds_bytes(const Plan& p) {
-    size_t tab = (size_t)round_up((int)p.tables.size() * 4, 16);
+    size_t tab = (size_t)table_lds_bytes(p);
     const int nbuf = p.stages.size() > 1 ? 2 : 1;
     return (size_t)nbuf * p.stage_max + tab + (size_t)p.samples_per_block * p.stride * 4;
 }
@@ -1058,7 +1058,7 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err, int exact
         }
 
         const int nbuf = P.stages.size() > 1 ? 2 : 1;
-        const int fixed = nbuf * P.stage_max + round_up((int)P.tables.size() * 4, 16);
+        const int fixed = nbuf * P.stage_max + table_lds_bytes(P);
         const int per_tile = kWavesPerBlock * 16 * P.stride * 4;
         P.tiles = 1;
         if (resident)
@@ -1073,7 +1073,8 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err, int exact
             P.tiles -= P.tiles % P.tile_group;
         }
         P.samples_per_block = kWavesPerBlock * 16 * P.tiles;
-        if ((int)P.tables.size() > kMaxTableInts) fail(DF_ERR_UNSUPPORTED, "chain index tables exceed 16 KiB");
+        if ((int)(P.tables.size() + P.params.size()) > kMaxTableInts)
+            fail(DF_ERR_UNSUPPORTED, "chain index tables and NormalizationLayer bounds exceed 16 KiB");
         if (P.stages.empty()) {  // normalization-only chain: keep one empty stage record
             P.stage_max = 0;
         }

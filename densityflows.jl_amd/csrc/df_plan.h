@@ -259,5 +259,8 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err, int exact
 
 // Workgroup LDS bytes for a plan (stage buffers + tables + state tile).
 size_t plan_lds_bytes(const Plan& p);
+// LDS bytes of the table area: the index tables, then the NormalizationLayer bounds
+// (`params`), which the specialised kernel copies next to them (ChainArgs::n_par).
+inline int table_lds_bytes(const Plan& p) { return (int)(((p.tables.size() + p.params.size()) * 4 + 15) / 16 * 16); }
 
 }  // namespace df

@@ -1,0 +1,302 @@
+// df_small.hip — the small-batch chain kernel.
+//
+// For a batch that leaves most of the chip idle (config 1 at its stated B = 4096:
+// 128 tiles of 32 samples for 1024 SIMDs) a launch lasts as long as ONE wave's
+// dependent chain through the layers.  The specialised kernel's chain is long
+// (profiles/r04_phase_cfg1.txt, in-kernel phase stamps of workgroup 0): three
+// serial global round trips to copy the tables and the state tile in, two LDS
+// round trips per feature read, coupling update and ldj update of every net, a
+// barrier per stage switch and before the copy-out.  This kernel removes all of
+// it: one wave per workgroup, two 16-sample tiles per wave, and
+//   * every lane holds the whole state row of its sample, vcat(θ, z) plus the
+//     zero slot and the 1 of the folded first-Dense bias, in registers; the
+//     conditioner features are register selects, the coupling updates the row
+//     in place (RNVP.jl:182-184 / 86-90), the ldj accumulators are registers;
+//   * the weight fragments of the next layer's nets are loaded from the blob (the
+//     same bytes the LDS stages hold) into registers while the current layer runs;
+//   * no LDS, no barrier; the outputs are stored from registers.
+// The arithmetic is the FAST variant's, operation for operation: the first Dense
+// as one f32 MFMA k-step with the bias folded in, the hidden Dense as the
+// k-ordered f32 MFMA chain, bias then relu, the output Dense as the VALU GEMV
+// reduced over lane groups as ((p0 + p1) + (p2 + p3)) then + b, the coupling
+// rounded as z·exp(s), + t (forward) and (x − t), ·exp(−s) (inverse), Σ s in row
+// order, the ldj grouped per FlowElement (Blocks.jl:136,149, Chains.jl:160,179) —
+// so its outputs are bitwise those of the FAST kernel.  The one difference is the
+// order of the fp64 NLL partial sums (per workgroup of 32 samples).
+#include "df_uniform_impl.h"
+
+namespace df {
+namespace small {
+
+constexpr int kStride = 13;  // LDS row of a sample: θ | z (n + d <= 8) | zero slot | 2 unused | 1 (folded bias)
+
+struct NetW {      // one FAST hidden-16 net's fragments (the stage layout of df_uniform_impl.h, HT = 1)
+    float w0;      // first Dense, KS = 1, bias folded: [lane]
+    f32x4 wh;      // hidden 16×16 Dense: [lane][4]
+    f32x4 bh;      // hidden bias, rows 4g ..
+    f32x4 wo[4];   // output Dense (<= 4 rows): row oo, columns 4g ..
+    float bo;      // output bias of lane group g's output (out_valu_t)
+};
+
+// net k (0 = s, 1 = t) of layer li: its fragments at the blob offsets of the descriptor
+__device__ __forceinline__ void load_net(const ChainArgs& a, const SmallDesc& sd, int li, int k, NetW& w) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    w.w0 = reinterpret_cast<const float*>(a.blob + sd.w0[li][k])[lane];
+    w.wh = *reinterpret_cast<const f32x4*>(a.blob + sd.wh[li][k] + lane * 16);
+    w.bh = *reinterpret_cast<const f32x4*>(a.blob + sd.wh[li][k] + 1024 + ((4 * g) << 2));
+    const uint8_t* w3 = a.blob + sd.wo[li][k];
+    const int no = sd.n_out[li];
+    // branch-free (one basic block for every net's loads, so they all issue before the
+    // first wait): rows past n_out repeat the last one and are never used
+#pragma unroll
+    for (int oo = 0; oo < 4; ++oo) {
+        const int r = oo < no ? oo : (no > 0 ? no - 1 : 0);
+        w.wo[oo] = *reinterpret_cast<const f32x4*>(w3 + ((r * 16 + 4 * g) << 2));
+    }
+    w.bo = reinterpret_cast<const float*>(w3)[no * 16 + (g < no ? g : 0)];
+}
+
+// One net on the wave's tile: y = output g of the lane's sample (lane groups g < NO).
+// The FAST kernel's functions operation for operation: dense_first (KS = 1, the bias
+// folded into k-slot 3), relu, dense_hidden (k-ordered f32 MFMA chain), bias + relu,
+// out_valu_t (GEMV, lane-group transpose, + b).
+template <int NO>
+__device__ __forceinline__ float eval_net(const NetW& w, float xin) {
+    f32x4 A = impl::mfma4(w.w0, xin, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+    for (int r = 0; r < 4; ++r) A[r] = uni::relu_fast(A[r]);
+    f32x4 B = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) B = impl::mfma4(w.wh[r], A[r], B);
+    B = B + w.bh;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) B[r] = uni::relu_fast(B[r]);
+    float p[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int oo = 0; oo < NO; ++oo)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[oo] = __builtin_fmaf(w.wo[oo][r], B[r], p[oo]);
+    auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(p[0]), __float_as_uint(p[1]), false, false);
+    const float A2 = __uint_as_float(x[0]) + __uint_as_float(x[1]);
+    float Bv = 0.f;
+    if constexpr (NO > 2) {
+        auto y = __builtin_amdgcn_permlane16_swap(__float_as_uint(p[2]), __float_as_uint(p[3]), false, false);
+        Bv = __uint_as_float(y[0]) + __uint_as_float(y[1]);
+    }
+    auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(A2), __float_as_uint(Bv), false, false);
+    return (__uint_as_float(c[0]) + __uint_as_float(c[1])) + w.bo;
+}
+
+template <int MODE, int NL>
+__global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd) {
+    constexpr bool FWD = (MODE == MODE_FWD || MODE == MODE_FWD_INPLACE);
+    constexpr bool WANT_LDJ = (MODE != MODE_FWD_INPLACE);
+    __shared__ float srow[16 * kStride];
+    ClockStamp clk;
+    clk.begin(a);
+#ifdef DF_PHASE_STAMPS  // diagnostic build (wrong outputs): wave 0 of workgroup 0 stamps its phases
+    uint64_t ph[12] = {};
+#define DF_PH(i) do { if (blockIdx.x == 0) ph[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define DF_PH(i) do {} while (0)
+#endif
+    DF_PH(0);
+    const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+    const int d = a.d, n = a.n, nd = n + d;
+    const int64_t smp = (int64_t)blockIdx.x * 16 + j;
+    const bool valid = smp < a.batch;
+    float* row = srow + j * kStride;
+
+    // every load in flight before the first use: the row (lane group g: columns g, g + 4,
+    // g + 8), then every coupling net's fragments
+    // branch-free: a clamped address always, the value selected afterwards
+    float rv[3];
+    const int64_t sv = valid ? smp : 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int c = g + 4 * q;
+        const bool is_th = c < n, is_z = c >= n && c < nd;
+        const float* p = is_th ? a.theta + sv * n + c : a.zin + sv * d + (is_z ? c - n : 0);
+        const float v = *p;
+        rv[q] = ((is_th || is_z) && valid) ? v : (c == nd + 3 ? 1.f : 0.f);
+    }
+    // every net's fragments (NormalizationLayers and NICE s-nets load the blob's first
+    // bytes, never used: the loads stay one basic block)
+    NetW ws[NL], wt[NL];
+#pragma unroll
+    for (int li = 0; li < NL; ++li) {
+        load_net(a, sd, li, 0, ws[li]);
+        load_net(a, sd, li, 1, wt[li]);
+    }
+    // the rest of the descriptor into the scalar cache now, under the vector loads: its
+    // fields are otherwise fetched on first use, one cache miss inside a layer each
+    {
+        const uint32_t* sdw = reinterpret_cast<const uint32_t*>(&sd);
+#pragma unroll
+        for (int l = 1; l < (int)((sizeof(SmallDesc) + 63) / 64); ++l) {
+            const uint32_t v = sdw[l * 16];
+            asm volatile("" ::"s"(v));
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int c = g + 4 * q;
+        float v = rv[q];
+        if (c < n && sd.norm_theta && valid) {  // normalize_input (Data.jl:213-218)
+            const float lo = sd.tmin[c], diff = sd.tmax[c] - lo;
+            v = (diff == 0.f) ? 0.f : (v - lo) / diff;
+        }
+        if (c < kStride) row[c] = v;
+    }
+    DF_PH(1);
+    float ldjA = 0.f, ldjE = 0.f;  // lane group 0: the sample's chain and element ldj
+    bool have_acc = false;
+    auto ldj_update = [&](float l, bool first_in_elem, bool last_in_elem) {
+        const float e = first_in_elem ? l : ldjE + l;
+        ldjE = e;
+        if (last_in_elem) ldjA = have_acc ? ldjA + e : e;
+    };
+
+#pragma unroll
+    for (int it = 0; it < NL; ++it) {
+        const int li = FWD ? it : NL - 1 - it;
+        const int kind = sd.kind[li];
+        const bool first_in_elem = FWD ? sd.elem_start[li] : sd.elem_end[li];
+        const bool last_in_elem = FWD ? sd.elem_end[li] : sd.elem_start[li];
+        if (kind == DF_LAYER_NORM) {  // src/norm/Normalization.jl:64-103
+            const float al = sd.alpha[li], be = sd.beta[li], delta = be - al;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int i = g + 4 * q;
+                if (i < d) {
+                    // lane group g's dims: the bounds by uniform index (register selects)
+                    const float lo = q == 0 ? (g == 0 ? sd.xmin[li][0] : g == 1 ? sd.xmin[li][1] : g == 2 ? sd.xmin[li][2]
+                                                                                                     : sd.xmin[li][3])
+                                            : (g == 0 ? sd.xmin[li][4] : g == 1 ? sd.xmin[li][5] : g == 2 ? sd.xmin[li][6]
+                                                                                                     : sd.xmin[li][7]);
+                    const float hi = q == 0 ? (g == 0 ? sd.xmax[li][0] : g == 1 ? sd.xmax[li][1] : g == 2 ? sd.xmax[li][2]
+                                                                                                     : sd.xmax[li][3])
+                                            : (g == 0 ? sd.xmax[li][4] : g == 1 ? sd.xmax[li][5] : g == 2 ? sd.xmax[li][6]
+                                                                                                     : sd.xmax[li][7]);
+                    const float xd = hi - lo;
+                    float v = row[n + i];
+                    if (FWD) v = ((xd * v - al * hi) + be * lo) / delta;
+                    else v = (be * (v - lo) + al * (hi - v)) / xd;
+                    row[n + i] = v;
+                }
+            }
+            ldj_update(FWD ? sd.ldj_const[li] : -sd.ldj_const[li], first_in_elem, last_in_elem);
+        } else {
+            const bool rnvp = (kind == DF_LAYER_RNVP);
+            const int fslot = g == 0 ? sd.feat[li][0] : g == 1 ? sd.feat[li][1] : g == 2 ? sd.feat[li][2] : sd.feat[li][3];
+            const float xin = row[fslot];
+            const int slot = g == 0 ? sd.af[li][0] : g == 1 ? sd.af[li][1] : g == 2 ? sd.af[li][2] : sd.af[li][3];
+            auto couple = [&](auto no_tag) {
+                constexpr int NO = decltype(no_tag)::value;
+                const float ys = rnvp ? eval_net<NO>(ws[li], xin) : 0.f;
+                const float yt = eval_net<NO>(wt[li], xin);
+                if (g < NO) {
+                    float v = row[slot];
+                    if (FWD) {
+                        if (rnvp) v = v * expf(ys);
+                        v = v + yt;
+                    } else {
+                        v = v - yt;
+                        if (rnvp) v = v * expf(-ys);
+                    }
+                    row[slot] = v;
+                }
+                // ldj = Σ_k s_k in row order (RNVP.jl:180 / :86), valid in lane group 0
+                const float sum = rnvp ? uni::group_row_sum<NO>(ys) : 0.f;
+                ldj_update(rnvp ? (FWD ? sum : -sum) : 0.f, first_in_elem, last_in_elem);
+            };
+            switch (sd.n_out[li]) {
+                case 1: couple(std::integral_constant<int, 1>{}); break;
+                case 2: couple(std::integral_constant<int, 2>{}); break;
+                case 3: couple(std::integral_constant<int, 3>{}); break;
+                default: couple(std::integral_constant<int, 4>{}); break;
+            }
+        }
+        have_acc = have_acc || last_in_elem;
+        DF_PH(2 + it);
+        if (!FWD && a.snap && valid) {  // training: every layer's output for the reverse sweep
+            float* dst = a.snap + (int64_t)li * a.batch * d;
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (g + 4 * q < d) dst[smp * d + g + 4 * q] = row[n + g + 4 * q];
+        }
+    }
+
+    if (MODE == MODE_LOGPDF) {
+        double part = 0.0;
+        if (g == 0) {
+            float q = 0.f;
+            for (int i = 0; i < d; ++i) {
+                const float zz = row[n + i];
+                q = q + zz * zz;
+            }
+            const float lp = (a.c0 - q / 2.f) + ldjA;
+            if (valid) {
+                if (a.lp_out) a.lp_out[smp] = lp;
+                part = (double)lp;
+            }
+        }
+        if (a.partial) {
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off);
+            if (lane == 0) a.partial[blockIdx.x] = part;
+        }
+        if (!a.xout) {
+            clk.end(a);
+            return;
+        }
+    }
+    if (valid) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (g + 4 * q < d) a.xout[smp * d + g + 4 * q] = row[n + g + 4 * q];
+        if (WANT_LDJ && MODE != MODE_LOGPDF && a.ldj_out && g == 0) a.ldj_out[smp] = ldjA;
+    }
+#ifdef DF_PHASE_STAMPS
+    DF_PH(6);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    DF_PH(7);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 1; i < 8; ++i) a.xout[i] = (float)(ph[i] - ph[0]);
+    }
+#endif
+#undef DF_PH
+    clk.end(a);
+}
+
+template <int MODE>
+void* kernel_ptr_m(int nl) {
+    switch (nl) {
+        case 1: return reinterpret_cast<void*>(&small_kernel<MODE, 1>);
+        case 2: return reinterpret_cast<void*>(&small_kernel<MODE, 2>);
+        case 3: return reinterpret_cast<void*>(&small_kernel<MODE, 3>);
+        case 4: return reinterpret_cast<void*>(&small_kernel<MODE, 4>);
+        default: return nullptr;
+    }
+}
+
+void* kernel_ptr(int mode, int nl) {
+    switch (mode) {
+        case MODE_FWD: return kernel_ptr_m<MODE_FWD>(nl);
+        case MODE_FWD_INPLACE: return kernel_ptr_m<MODE_FWD_INPLACE>(nl);
+        case MODE_BWD: return kernel_ptr_m<MODE_BWD>(nl);
+        default: return kernel_ptr_m<MODE_LOGPDF>(nl);
+    }
+}
+
+}  // namespace small
+
+hipError_t launch_small(int mode, const ChainArgs& a, const SmallDesc& sd, unsigned grid, hipStream_t st) {
+    void* f = small::kernel_ptr(mode, a.n_layers);
+    if (!f) return hipErrorInvalidValue;
+    void* args[] = {const_cast<ChainArgs*>(&a), const_cast<SmallDesc*>(&sd)};
+    return hipLaunchKernel(f, dim3(grid), dim3(64), args, 0, st);
+}
+
+}  // namespace df

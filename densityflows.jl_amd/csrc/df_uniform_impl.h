@@ -614,6 +614,52 @@ __device__ __forceinline__ void net_tiles(const uint8_t* buf, const UNet& N, con
     else tail<HT, TT, OUTV, RELU, PH, NO>(buf, N, L, tab, state, ro, sum, B);
 }
 
+// The s-net and t-net of one RNVP layer evaluated together (FAST variant, exact f32,
+// both nets in the resident stage, NO = n_af outputs each): they read the same
+// conditioner features (vcat(θ,z)[axis_nn], RNVP.jl:174-177), so their MFMA chains and
+// GEMV tails are independent and interleave, which halves the dependent latency of a
+// layer for a wave that has no other work (small batches: profiles/r04_phase_cfg1.txt).
+// The coupling is then applied in the reference's order with the same roundings as the
+// two phases of net_tiles: forward z·exp(s) then + t (RNVP.jl:182-184), inverse (x − t)
+// then ·exp(−s) (RNVP.jl:86-90); ssum[t] = Σ_k s_k in row order (lane group 0).
+template <int HT, int TT, bool RELU, bool FWDP, int NO>
+__device__ __forceinline__ void net_pair_tiles(const uint8_t* buf, const ULayer& L, const int32_t* tab, float* state,
+                                               const int (&ro)[TT], float (&ssum)[TT]) {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    float xin[TT][4];
+    const int slot_in = tab[L.feat_tab + g];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) xin[t][0] = state[ro[t] + slot_in];
+    f32x4 As[TT][HT], At[TT][HT], Bs[TT][HT], Bt[TT][HT];
+    dense_first<HT, TT, 1>(buf, L.s, xin, As);
+    dense_first<HT, TT, 1>(buf, L.t, xin, At);
+    bias_act<HT, TT, RELU>(buf + L.s.off_b0, L.s.act0, As, false);
+    bias_act<HT, TT, RELU>(buf + L.t.off_b0, L.t.act0, At, false);
+    dense_hidden<HT, TT>(buf + L.s.off_h, As, Bs);
+    dense_hidden<HT, TT>(buf + L.t.off_h, At, Bt);
+    bias_act<HT, TT, RELU>(buf + L.s.off_h + HT * HT * 1024, L.s.acth, Bs);
+    bias_act<HT, TT, RELU>(buf + L.t.off_h + HT * HT * 1024, L.t.acth, Bt);
+    float ys[TT], yt[TT];
+    out_valu_t<HT, TT, NO>(buf, L.s, Bs, ys);
+    out_valu_t<HT, TT, NO>(buf, L.t, Bt, yt);
+    const int slot = tab[L.af_tab + (g < NO ? g : 0)];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+        if (g < NO) {
+            float v = state[ro[t] + slot];
+            if (FWDP) {
+                v = v * expf(ys[t]);
+                v = v + yt[t];
+            } else {
+                v = v - yt[t];
+                v = v * expf(-ys[t]);
+            }
+            state[ro[t] + slot] = v;
+        }
+        ssum[t] = group_row_sum<NO>(ys[t]);
+    }
+}
+
 }  // namespace uni
 
 #ifndef DF_UNI_WAVES
@@ -637,6 +683,13 @@ uniform_kernel(ChainArgs a) {
 
     ClockStamp clk;
     clk.begin(a);
+#ifdef DF_PHASE_STAMPS  // diagnostic build (wrong outputs): wave 0 of workgroup 0 stamps its phases
+    uint64_t ph[16] = {};
+#define DF_PH(i) do { if (blockIdx.x == 0 && threadIdx.x == 0) ph[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define DF_PH(i) do {} while (0)
+#endif
+    DF_PH(0);
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, j = lane & 15;
@@ -654,30 +707,108 @@ uniform_kernel(ChainArgs a) {
     sg.n = FWD ? a.n_sched_fwd : a.n_sched_bwd;
     impl::stager_start(sg, a);
 
-    for (int i = tid; i < a.tab_ints; i += kBlockThreads) tab[i] = a.tables[i];
-    for (int i = tid; i < S * d; i += kBlockThreads) {
-        const int smp = i / d, c = i - smp * d;
-        float v = 0.f;
-        if (smp < nvalid) v = a.zin[(s0 + smp) * d + c];
-        state[smp * stride + n + c] = v;
-    }
-    for (int i = tid; i < S * n; i += kBlockThreads) {
-        const int smp = i / n, c = i - smp * n;
-        float v = 0.f;
-        if (smp < nvalid) {
-            v = a.theta[(s0 + smp) * n + c];
-            if (a.tmin) {  // normalize_input (Data.jl:213-218)
-                const float lo = a.tmin[c], diff = a.tmax[c] - lo;
-                v = (diff == 0.f) ? 0.f : (v - lo) / diff;
-            }
+    // Copy-in of the tables, the NormalizationLayer bounds (a.params, kept in LDS right
+    // after the tables) and the state tile.  Fast form: every thread issues ALL its loads
+    // — up to four table words, one bound, one θ bound per lane, its sample row's z and
+    // θ — before its first LDS store, so the copy costs one memory latency; three serial
+    // load → store loops cost three (≈1.5 k cycles each, profiles/r04_phase_cfg1.txt),
+    // which is a third of a config-1 launch at B = 4096.
+    float* tabf = reinterpret_cast<float*>(tab);
+    constexpr int kRowMax = 8;  // fast copy-in: d, n <= 8 (every default-shape chain of the configs)
+    const bool fast_copy = d <= kRowMax && n <= kRowMax && a.n_par <= kBlockThreads && a.tab_ints <= 4 * kBlockThreads;
+    auto row_init = [&](int smp) {  // [0 | ldj_chain | ldj_elem | 1 (folded-bias input)]
+        for (int c = nd; c < stride; ++c) state[smp * stride + c] = (c == nd + 3) ? 1.f : 0.f;
+    };
+    auto theta_in = [&](float v, float lo, float hi) {  // normalize_input (Data.jl:213-218)
+        const float diff = hi - lo;
+        return (diff == 0.f) ? 0.f : (v - lo) / diff;
+    };
+    if (fast_copy) {
+        const int n_tab = a.tab_ints, n_par = a.n_par;
+        int tv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = tid + u * kBlockThreads;
+            tv[u] = i < n_tab ? a.tables[i] : 0;
         }
-        state[smp * stride + c] = v;
+        const float pv = tid < n_par ? a.params[tid] : 0.f;
+        const bool norm_th = a.tmin != nullptr;
+        const float blo = (norm_th && lane < n) ? a.tmin[lane] : 0.f;  // lane c: column c's bounds
+        const float bhi = (norm_th && lane < n) ? a.tmax[lane] : 0.f;
+        const int smp = tid;                                           // this thread's first row
+        const bool valid = smp < nvalid;
+        float zr[kRowMax], tr[kRowMax];
+#pragma unroll
+        for (int c = 0; c < kRowMax; ++c)
+            if (c < d) zr[c] = valid ? a.zin[(s0 + smp) * d + c] : 0.f;
+#pragma unroll
+        for (int c = 0; c < kRowMax; ++c)
+            if (c < n) tr[c] = valid ? a.theta[(s0 + smp) * n + c] : 0.f;
+        // every load is in flight: the stores
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = tid + u * kBlockThreads;
+            if (i < n_tab) tab[i] = tv[u];
+        }
+        if (tid < n_par) tabf[n_tab + tid] = pv;
+#pragma unroll
+        for (int c = 0; c < kRowMax; ++c)
+            if (c < n) {
+                const float lo = __shfl(blo, c), hi = __shfl(bhi, c);
+                if (smp < S) state[smp * stride + c] = (norm_th && valid) ? theta_in(tr[c], lo, hi) : tr[c];
+            }
+        if (smp < S) {
+#pragma unroll
+            for (int c = 0; c < kRowMax; ++c)
+                if (c < d) state[smp * stride + n + c] = zr[c];
+            row_init(smp);
+        }
+        // rows beyond the first kBlockThreads (tiles > 4): element by element
+        for (int i = tid + kBlockThreads * d; i < S * d; i += kBlockThreads) {
+            const int r = i / d, c = i - r * d;
+            state[r * stride + n + c] = r < nvalid ? a.zin[(s0 + r) * d + c] : 0.f;
+        }
+        for (int i = tid + kBlockThreads * n; i < S * n; i += kBlockThreads) {
+            const int r = i / n, c = i - r * n;
+            float v = 0.f;
+            if (r < nvalid) {
+                v = a.theta[(s0 + r) * n + c];
+                if (norm_th) v = theta_in(v, a.tmin[c], a.tmax[c]);
+            }
+            state[r * stride + c] = v;
+        }
+        for (int r = tid + kBlockThreads; r < S; r += kBlockThreads) row_init(r);
+    } else {
+        for (int i = tid; i < a.tab_ints; i += kBlockThreads) tab[i] = a.tables[i];
+        for (int i = tid; i < S * d; i += kBlockThreads) {
+            const int smp = i / d, c = i - smp * d;
+            float v = 0.f;
+            if (smp < nvalid) v = a.zin[(s0 + smp) * d + c];
+            state[smp * stride + n + c] = v;
+        }
+        for (int i = tid; i < S * n; i += kBlockThreads) {
+            const int smp = i / n, c = i - smp * n;
+            float v = 0.f;
+            if (smp < nvalid) {
+                v = a.theta[(s0 + smp) * n + c];
+                if (a.tmin) v = theta_in(v, a.tmin[c], a.tmax[c]);
+            }
+            state[smp * stride + c] = v;
+        }
+        for (int i = tid; i < S; i += kBlockThreads) row_init(i);
     }
-    for (int i = tid; i < S; i += kBlockThreads)  // [0 | ldj_chain | ldj_elem | 1 (folded-bias input)]
-        for (int c = nd; c < stride; ++c) state[i * stride + c] = (c == nd + 3) ? 1.f : 0.f;
+    DF_PH(1);
+    DF_PH(2);
+    DF_PH(3);
     __syncthreads();
+    DF_PH(4);
 
     const int row0 = ((wave * nt) * 16 + j) * stride;  // tile tt: row0 + tt*16*stride
+#ifdef DF_NO_PAIR  // A/B build: the s and t nets of a layer one after the other
+    constexpr bool no_pair = true;
+#else
+    constexpr bool no_pair = false;
+#endif
     const int tstep = 16 * stride;
     bool have_acc = false;
 
@@ -693,25 +824,34 @@ uniform_kernel(ChainArgs a) {
         // descriptors through the constant address space: scalar loads (the host
         // writes them before the launch; nothing in the kernel stores to them)
         using CULayer = const __attribute__((address_space(4))) ULayer;
+#ifdef DF_PHASE_STAMPS  // diagnostic: the whole descriptor loaded (and waited for) up front
+        const ULayer L = *(const ULayer*)(&((CULayer*)(uintptr_t)a.ulayers)[li]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (it == 1) DF_PH(13);
+#else
         const ULayer& L = *(const ULayer*)(&((CULayer*)(uintptr_t)a.ulayers)[li]);
+#endif
         const int kind = L.kind;
         const bool first_in_elem = FWD ? L.elem_start : L.elem_end;
         const bool last_in_elem = FWD ? L.elem_end : L.elem_start;
         if (kind == DF_LAYER_NORM) {
             const float al = L.alpha, be = L.beta, delta = be - al;
-            const float* xmn = a.params + L.norm_off;
-            const float* xmx = xmn + d;
-            for (int tt = 0; tt < nt; ++tt) {
-                const int ro = row0 + tt * tstep;
-                for (int i = g; i < d; i += 4) {
-                    const float lo = xmn[i], hi = xmx[i], xd = hi - lo;
-                    float v = state[ro + n + i];
-                    if (FWD) v = ((xd * v - al * hi) + be * lo) / delta;
-                    else v = (be * (v - lo) + al * (hi - v)) / xd;
-                    state[ro + n + i] = v;
+            auto norm = [&](const auto* xmn) {
+                const auto* xmx = xmn + d;
+                for (int tt = 0; tt < nt; ++tt) {
+                    const int ro = row0 + tt * tstep;
+                    for (int i = g; i < d; i += 4) {
+                        const float lo = xmn[i], hi = xmx[i], xd = hi - lo;
+                        float v = state[ro + n + i];
+                        if (FWD) v = ((xd * v - al * hi) + be * lo) / delta;
+                        else v = (be * (v - lo) + al * (hi - v)) / xd;
+                        state[ro + n + i] = v;
+                    }
+                    ldj_update(ro, FWD ? L.ldj_const : -L.ldj_const, first_in_elem, last_in_elem);
                 }
-                ldj_update(ro, FWD ? L.ldj_const : -L.ldj_const, first_in_elem, last_in_elem);
-            }
+            };
+            if (fast_copy) norm(tabf + a.tab_ints + L.norm_off);  // the bounds were copied to LDS
+            else norm(a.params + L.norm_off);
         } else {
             const bool rnvp = (kind == DF_LAYER_RNVP);
             // this wave's tiles in groups of kTT (nt is a multiple of kTT)
@@ -750,8 +890,43 @@ uniform_kernel(ChainArgs a) {
             using PTF = std::integral_constant<int, impl::PH_T_FWD>;
             using PTB = std::integral_constant<int, impl::PH_T_BWD>;
             using PSB = std::integral_constant<int, impl::PH_S_BWD>;
-            if (FWD) {
+            bool paired = false;
+            if constexpr (FAST && OUTV && !SPLIT && HT <= 2) {
+                // s and t together when both sit in one stage with the same output count
+                if (rnvp && L.s.stage == L.t.stage && L.s.n_out == L.t.n_out && !no_pair) {
+                    impl::ensure_stage(L.s.stage, sg, a);
+                    auto pair_loop = [&](auto no_tag) {
+                        constexpr int NO = decltype(no_tag)::value;
+                        const uint8_t* buf = sg.buf();
+                        for (int tt = 0; tt < nt; tt += kTT) {
+                            int ro[kTT];
+                            float ssum[kTT];
+#pragma unroll
+                            for (int t = 0; t < kTT; ++t) ro[t] = row0 + (tt + t) * tstep;
+                            net_pair_tiles<HT, kTT, RELU, FWD, NO>(buf, L, tab, state, ro, ssum);
+#pragma unroll
+                            for (int t = 0; t < kTT; ++t)
+                                ldj_update(ro[t], FWD ? ssum[t] : -ssum[t], first_in_elem, last_in_elem);
+                        }
+                    };
+                    switch (L.s.n_out) {
+                        case 1: pair_loop(std::integral_constant<int, 1>{}); break;
+                        case 2: pair_loop(std::integral_constant<int, 2>{}); break;
+                        case 3: pair_loop(std::integral_constant<int, 3>{}); break;
+                        default: pair_loop(std::integral_constant<int, 4>{}); break;
+                    }
+                    paired = true;
+                }
+            }
+            if (paired) {
+            } else if (FWD) {
+#ifdef DF_PHASE_STAMPS
+                if (it == 1) DF_PH(11);
+#endif
                 if (rnvp) run_net(L.s, PSF{}, true, 1.f);
+#ifdef DF_PHASE_STAMPS
+                if (it == 1) DF_PH(12);
+#endif
                 run_net(L.t, PTF{}, false, 1.f);
             } else {
                 run_net(L.t, PTB{}, false, 1.f);
@@ -759,6 +934,12 @@ uniform_kernel(ChainArgs a) {
             }
         }
         have_acc = have_acc || last_in_elem;
+#ifdef DF_PHASE_STAMPS
+        if (it == 0) DF_PH(5);
+        if (it == 1) DF_PH(6);
+        if (it == 2) DF_PH(7);
+        if (it == 3) DF_PH(8);
+#endif
         if (!FWD && a.snap) {  // training: keep every layer's output for the reverse sweep
             float* dst = a.snap + (int64_t)li * a.batch * d;
             for (int tt = 0; tt < nt; ++tt) {
@@ -814,6 +995,16 @@ uniform_kernel(ChainArgs a) {
     if (WANT_LDJ && MODE != MODE_LOGPDF && a.ldj_out) {
         for (int i = tid; i < nvalid; i += kBlockThreads) a.ldj_out[s0 + i] = state[i * stride + cA];
     }
+    DF_PH(9);
+#ifdef DF_PHASE_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    DF_PH(10);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 1; i < 14; ++i) a.xout[i] = (float)(ph[i] - ph[0]);
+    }
+#endif
+#undef DF_PH
     clk.end(a);
 }
 

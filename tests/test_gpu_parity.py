@@ -181,12 +181,14 @@ def _fast_case_chain(case, rng):
 @pytest.mark.parametrize("case", ["af1_h64", "af4_h64", "in4_h64", "nice_h32", "block_h16"])
 def test_fast_variant_cases(cuda, case, monkeypatch, capfd):
     """FAST-variant tails for every output count: against the fp64 oracle, and
-    bitwise against the non-FAST / unfolded plans of the same chain."""
+    bitwise against the non-FAST / unfolded plans of the same chain; the small-batch
+    kernel (hidden 16 / 32) bitwise against the FAST kernel (DF_SMALL_MAX=0)."""
     import bench
 
     outs = []
-    for env in ({"DF_DEBUG_LAUNCH": "1"}, {"DF_NO_FAST": "1"}, {"DF_NO_FOLD": "1"}, {"SPLIT": "1"}):
-        for k in ("DF_NO_FAST", "DF_NO_FOLD", "DF_DEBUG_LAUNCH", "DF_F32_EXACT"):
+    for env in ({"DF_DEBUG_LAUNCH": "1"}, {"DF_DEBUG_LAUNCH": "1", "DF_SMALL_MAX": "0"}, {"DF_NO_FAST": "1"},
+                {"DF_NO_FOLD": "1"}, {"SPLIT": "1"}):
+        for k in ("DF_NO_FAST", "DF_NO_FOLD", "DF_DEBUG_LAUNCH", "DF_F32_EXACT", "DF_SMALL_MAX"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             if k != "SPLIT":
@@ -216,7 +218,11 @@ def test_fast_variant_cases(cuda, case, monkeypatch, capfd):
 
             torch.cuda.synchronize()
             launches = capfd.readouterr().err
-            want = "kernel uniform " if case == "in4_h64" else "kernel uniform-fast "
+            # hidden-16 FAST chains of <= 4 layers at this batch run the small-batch kernel (df_small.hip),
+            # whose outputs are bitwise the FAST kernel's (the comparisons below)
+            small = case == "block_h16" and "DF_SMALL_MAX" not in env
+            want = ("kernel uniform " if case == "in4_h64" else "kernel small " if small else
+                    "kernel uniform-fast ")
             assert want in launches, launches
             xo, lo = O.forward(chain.to_spec(), z, th if n else np.zeros((0, B), np.float32), np.float64)
             assert close(_np(x), xo, RTOL)[0] and close(_np(lf), lo, RTOL)[0]
@@ -636,3 +642,50 @@ def test_chain_set_weights(cuda):
     wrong = dfa.FlowChain(dfa.CouplingLayer(5, [1, 2, 3], n=1, hidden_dim=32, rng=rng))
     with pytest.raises((AssertionError, dfa.ArgumentError)):
         hc.set_weights(wrong.layers)
+
+
+@pytest.mark.parametrize("B", [1, 31, 32, 33, 4096, 5000])
+def test_small_kernel_bitwise_fast_kernel(cuda, B, monkeypatch, capfd):
+    """The small-batch kernel (df_small.hip: state rows in registers, weights loaded
+    from the blob, no LDS) against the FAST kernel it replaces at small batches
+    (DF_SMALL_MAX=0): forward, forward!, inverse, per-sample logpdf and the inverse
+    pass's per-layer outputs (training snapshots, via a gradient) bitwise; the
+    fp64 Σ logpdf to rounding of its summation order."""
+    import torch
+
+    from densityflows_amd.train import Adam, HIPTrainer
+
+    spec, g, meta = G.load("cfg1")
+    z = np.ascontiguousarray(g["z"][:, :B]) if B <= g["z"].shape[1] else \
+        np.random.default_rng(B).standard_normal((5, B)).astype(np.float32)
+    th = np.random.default_rng(B + 1).uniform(-1, 2, (1, B)).astype(np.float32)
+    res = {}
+    for mode in ("small", "fast"):
+        monkeypatch.delenv("DF_SMALL_MAX", raising=False)
+        if mode == "fast":
+            monkeypatch.setenv("DF_SMALL_MAX", "0")
+        monkeypatch.setenv("DF_DEBUG_LAUNCH", "1")
+        chain = spec_to_element(spec)
+        flow = dfa.Flow(chain, metadata=dfa.MetaData("", 5, 1, g["theta_min"], g["theta_max"]))
+        x, lf = dfa.forward(chain, _t(z, cuda), _t(th, cuda))
+        zb, lb = dfa.backward(chain, x, _t(th, cuda))
+        zz = _t(z, cuda).clone()
+        flow.forward_(zz, _t(th, cuda))
+        lp = dfa.logpdf(flow, x, _t(th, cuda))
+        s, _ = flow.hip().logpdf_sum(x, _t(th, cuda))
+        tr = HIPTrainer(chain.hip(), Adam())
+        lps = torch.zeros(1, dtype=torch.float64, device=cuda)
+        xflat = x.T.contiguous().reshape(-1)
+        tr.gradient(xflat, _t(th, cuda).T.contiguous().reshape(-1), B, B, lps)
+        torch.cuda.synchronize()
+        launches = capfd.readouterr().err
+        assert ("kernel small " in launches) == (mode == "small"), launches
+        res[mode] = ([_np(v) for v in (x, lf, zb, lb, zz, lp)], float(s.item()), tr.grad().cpu().numpy().copy(),
+                     float(lps.item()))
+        monkeypatch.delenv("DF_DEBUG_LAUNCH", raising=False)
+    for a, b in zip(res["small"][0], res["fast"][0]):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_allclose(res["small"][1], res["fast"][1], rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(res["small"][3], res["fast"][3], rtol=1e-12, atol=1e-9)
+    # the gradient reads the inverse pass's snapshots: equal snapshots → equal gradient
+    np.testing.assert_array_equal(res["small"][2], res["fast"][2])
