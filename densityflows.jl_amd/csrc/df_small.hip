@@ -38,6 +38,25 @@ struct NetW {      // one FAST hidden-16 net's fragments (the stage layout of df
     float bo;      // output bias of lane group g's output (out_valu_t)
 };
 
+// A descriptor field as a scalar register.  The per-lane-group selects below would
+// otherwise be folded into ONE vector load from the kernel-argument segment at a
+// lane-dependent offset — a full memory round trip inside the layer.
+template <typename T>
+__device__ __forceinline__ T sreg(T v) {
+    asm("" : "+s"(v));
+    return v;
+}
+
+// v[g] for lane group g of four scalar values (register selects)
+template <typename T>
+__device__ __forceinline__ T by_group(int g, T v0, T v1, T v2, T v3) {
+    v0 = sreg(v0);
+    v1 = sreg(v1);
+    v2 = sreg(v2);
+    v3 = sreg(v3);
+    return g == 0 ? v0 : g == 1 ? v1 : g == 2 ? v2 : v3;
+}
+
 // net k (0 = s, 1 = t) of layer li: its fragments at the blob offsets of the descriptor
 __device__ __forceinline__ void load_net(const ChainArgs& a, const SmallDesc& sd, int li, int k, NetW& w) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
@@ -128,22 +147,17 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
         load_net(a, sd, li, 0, ws[li]);
         load_net(a, sd, li, 1, wt[li]);
     }
-    // the rest of the descriptor into the scalar cache now, under the vector loads: its
-    // fields are otherwise fetched on first use, one cache miss inside a layer each
-    {
-        const uint32_t* sdw = reinterpret_cast<const uint32_t*>(&sd);
-#pragma unroll
-        for (int l = 1; l < (int)((sizeof(SmallDesc) + 63) / 64); ++l) {
-            const uint32_t v = sdw[l * 16];
-            asm volatile("" ::"s"(v));
-        }
-    }
+
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
         const int c = g + 4 * q;
         float v = rv[q];
         if (c < n && sd.norm_theta && valid) {  // normalize_input (Data.jl:213-218)
-            const float lo = sd.tmin[c], diff = sd.tmax[c] - lo;
+            const float lo = q == 0 ? by_group(g, sd.tmin[0], sd.tmin[1], sd.tmin[2], sd.tmin[3])
+                                    : by_group(g, sd.tmin[4], sd.tmin[5], sd.tmin[6], sd.tmin[7]);
+            const float hi = q == 0 ? by_group(g, sd.tmax[0], sd.tmax[1], sd.tmax[2], sd.tmax[3])
+                                    : by_group(g, sd.tmax[4], sd.tmax[5], sd.tmax[6], sd.tmax[7]);
+            const float diff = hi - lo;
             v = (diff == 0.f) ? 0.f : (v - lo) / diff;
         }
         if (c < kStride) row[c] = v;
@@ -170,14 +184,10 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
                 const int i = g + 4 * q;
                 if (i < d) {
                     // lane group g's dims: the bounds by uniform index (register selects)
-                    const float lo = q == 0 ? (g == 0 ? sd.xmin[li][0] : g == 1 ? sd.xmin[li][1] : g == 2 ? sd.xmin[li][2]
-                                                                                                     : sd.xmin[li][3])
-                                            : (g == 0 ? sd.xmin[li][4] : g == 1 ? sd.xmin[li][5] : g == 2 ? sd.xmin[li][6]
-                                                                                                     : sd.xmin[li][7]);
-                    const float hi = q == 0 ? (g == 0 ? sd.xmax[li][0] : g == 1 ? sd.xmax[li][1] : g == 2 ? sd.xmax[li][2]
-                                                                                                     : sd.xmax[li][3])
-                                            : (g == 0 ? sd.xmax[li][4] : g == 1 ? sd.xmax[li][5] : g == 2 ? sd.xmax[li][6]
-                                                                                                     : sd.xmax[li][7]);
+                    const float lo = by_group(g, sd.xmin[li][4 * q], sd.xmin[li][4 * q + 1], sd.xmin[li][4 * q + 2],
+                                              sd.xmin[li][4 * q + 3]);
+                    const float hi = by_group(g, sd.xmax[li][4 * q], sd.xmax[li][4 * q + 1], sd.xmax[li][4 * q + 2],
+                                              sd.xmax[li][4 * q + 3]);
                     const float xd = hi - lo;
                     float v = row[n + i];
                     if (FWD) v = ((xd * v - al * hi) + be * lo) / delta;
@@ -188,9 +198,9 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
             ldj_update(FWD ? sd.ldj_const[li] : -sd.ldj_const[li], first_in_elem, last_in_elem);
         } else {
             const bool rnvp = (kind == DF_LAYER_RNVP);
-            const int fslot = g == 0 ? sd.feat[li][0] : g == 1 ? sd.feat[li][1] : g == 2 ? sd.feat[li][2] : sd.feat[li][3];
+            const int fslot = by_group<int>(g, sd.feat[li][0], sd.feat[li][1], sd.feat[li][2], sd.feat[li][3]);
             const float xin = row[fslot];
-            const int slot = g == 0 ? sd.af[li][0] : g == 1 ? sd.af[li][1] : g == 2 ? sd.af[li][2] : sd.af[li][3];
+            const int slot = by_group<int>(g, sd.af[li][0], sd.af[li][1], sd.af[li][2], sd.af[li][3]);
             auto couple = [&](auto no_tag) {
                 constexpr int NO = decltype(no_tag)::value;
                 const float ys = rnvp ? eval_net<NO>(ws[li], xin) : 0.f;
