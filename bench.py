@@ -339,8 +339,17 @@ def main():
                 raise
             comm_error = f"{type(e).__name__}: {e}"
     if args.mode == "forward":
+        # the C-ABI call with its arguments bound once (the stream does not change): the
+        # step is the library's host path + launch, not Python argument marshalling
+        import ctypes as C
+        from densityflows_amd.hip import _ptr, _stream
+        fwd = hc.lib.df_chain_forward
+        fwd_args = (hc.handle, _ptr(zbuf), _ptr(thbuf), _ptr(xbuf), _ptr(ldj), C.c_int64(B), _stream(dev))
+
         def step():
-            hc.run("forward", zbuf, thbuf, xbuf, ldj, B)
+            rc = fwd(*fwd_args)
+            if rc != 0:
+                raise RuntimeError(hc.lib.df_last_error().decode())
     elif args.mode == "train":
         # one train! step (src/Flows.jl:398-413) on a fixed synthetic batch: inverse pass,
         # reverse sweep, gradient all-reduce across ranks (RCCL), Adam, weight repack

@@ -102,8 +102,7 @@ static bool use_small(const df_chain* c, int64_t batch) {
     const df::Plan& P = c->plan;
     if (!(P.uniform && P.fast && P.outv && P.ht == 1 && P.n + P.d <= 8 && P.n_layers <= df::kSmallLayers))
         return false;
-    int64_t max_b = (int64_t)df::kSmallSamples * 8 * c->n_cu;
-    if (const char* e = std::getenv("DF_SMALL_MAX")) max_b = std::atoll(e);
+    const int64_t max_b = c->small_max >= 0 ? c->small_max : (int64_t)df::kSmallSamples * 8 * c->n_cu;
     return batch <= max_b;
 }
 
@@ -122,8 +121,8 @@ static int choose_tiles(const df_chain* c, int mode, int64_t batch, bool split) 
     const df::Plan& P = c->plan;
     const int max_t = split ? P.stiles : P.tiles;
     const int (*occ)[df::kMaxTilesPerWave + 1] = split ? c->socc : c->occ;
-    if (const char* e = std::getenv("DF_TILES")) {  // tuning knob: force the tiles per wave
-        const int t = std::atoi(e);
+    if (c->force_tiles > 0) {  // tuning knob (DF_TILES): force the tiles per wave
+        const int t = c->force_tiles;
         const int step = P.uniform ? P.tile_group : 1;
         if (t >= 1 && t <= max_t && t % step == 0) return t;
     }
@@ -198,6 +197,10 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
     std::string err;
     const char* ex = std::getenv("DF_F32_EXACT");   // the chain's arithmetic, read once
     c->exact = ex && ex[0] == '1';
+    c->no_wide = std::getenv("DF_NO_WIDE") && std::getenv("DF_NO_WIDE")[0] == '1';
+    c->debug_launch = std::getenv("DF_DEBUG_LAUNCH") && std::getenv("DF_DEBUG_LAUNCH")[0] == '1';
+    if (const char* e = std::getenv("DF_TILES")) c->force_tiles = std::atoi(e);
+    if (const char* e = std::getenv("DF_SMALL_MAX")) c->small_max = std::max<int64_t>(0, std::atoll(e));
     int rc = df::build_plan(desc, &c->plan, &err, c->exact ? 1 : 0);
     if (rc != DF_OK) {
         delete c;
@@ -410,6 +413,7 @@ int df_chain_set_weights(df_chain* c, const df_chain_desc* desc) {
     c->plan.wslayers = P.wslayers;
     c->plan.wsblob.swap(P.wsblob);
     c->plan.trainables.swap(P.trainables);
+    c->small_sd_ok[0] = c->small_sd_ok[1] = false;
     return DF_OK;
 }
 
@@ -429,6 +433,7 @@ int df_chain_set_theta_bounds(df_chain* c, const float* tmin, const float* tmax)
     if (e != hipSuccess) return hip_err(e, "hipMemcpy(θ bounds)");
     c->h_bounds = b;
     c->has_bounds = true;
+    c->small_sd_ok[1] = false;
     return DF_OK;
 }
 
@@ -458,12 +463,12 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
 
     DeviceGuard gd(c->device);
     if (!gd.ok) return set_err(DF_ERR_HIP, "hipSetDevice failed");
-    const bool wide = P.wide && !(std::getenv("DF_NO_WIDE") && std::getenv("DF_NO_WIDE")[0] == '1');
+    const bool wide = P.wide && !c->no_wide;
     const bool split = !wide && use_split(c);
     const bool small = !wide && !split && use_small(c, batch);
     const int tiles = wide ? df::kWideT : small ? 2 : choose_tiles(c, mode, batch, split);
-    if (const char* dbg = std::getenv("DF_DEBUG_LAUNCH")) {  // tuning aid: the launch shape on stderr
-        if (dbg[0] == '1') {
+    {
+        if (c->debug_launch) {  // tuning aid (DF_DEBUG_LAUNCH=1): the launch shape on stderr
             std::fprintf(stderr, "[df] mode %d batch %lld kernel %s tiles %d (max %d) occupancy:", mode,
                          (long long)batch,
                          wide ? (use_wsplit(c) ? "wide-split" : "wide") : small ? "small" : !P.uniform ? "generic" : split ? "uniform-fast-split" : P.fast ? "uniform-fast" : "uniform",
@@ -570,7 +575,12 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
             e = df::launch_wide(mode, a, (unsigned)grid, c->wide_lds, st);
         }
     } else if (small) {
-        e = df::launch_small(mode, a, small_desc(c, flow), (unsigned)grid, st);
+        const int fi = flow ? 1 : 0;
+        if (!c->small_sd_ok[fi]) {
+            c->small_sd[fi] = small_desc(c, flow);
+            c->small_sd_ok[fi] = true;
+        }
+        e = df::launch_small(mode, a, c->small_sd[fi], (unsigned)grid, st);
     } else if (split) {
         a.blob = static_cast<const uint8_t*>(c->d_sblob);
         a.stages = static_cast<const df::DevStage*>(c->d_sstages);

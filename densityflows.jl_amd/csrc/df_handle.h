@@ -16,6 +16,16 @@ struct df_chain {
     df::Plan plan;
     int device = 0;
     bool exact = false;         // DF_F32_EXACT=1 at df_chain_create: exact-f32 kernels only (read once)
+    // launch knobs, read from the environment once at df_chain_create (a launch does no
+    // getenv): DF_NO_WIDE=1, DF_DEBUG_LAUNCH=1, DF_TILES, DF_SMALL_MAX (-1: unset)
+    bool no_wide = false;
+    bool debug_launch = false;
+    int force_tiles = 0;
+    int64_t small_max = -1;
+    // the small-batch kernel's descriptor, by flow (θ normalised) 0 / 1; rebuilt after
+    // df_chain_set_weights / df_chain_set_theta_bounds
+    df::SmallDesc small_sd[2] = {};
+    bool small_sd_ok[2] = {false, false};
     void* d_layers = nullptr;
     void* d_denses = nullptr;
     void* d_chunks = nullptr;

@@ -32,6 +32,13 @@ constexpr int kLChunkBytes = 32 * 1024;  // weight chunk (LDS, double-buffered)
 #define DF_LTILES 2
 #endif
 constexpr int kLTiles = DF_LTILES;       // 16-sample tiles per wave per round
+#ifndef DF_LDENSE_SPLIT_1W
+#define DF_LDENSE_SPLIT_1W 1
+#endif
+// SPLIT (hidden-256 W1ᵀδ1) instances: waves per workgroup × tiles per wave (samples per
+// workgroup round = kWavesPerBlock · kLTiles either way)
+constexpr int kSplitWaves = DF_LDENSE_SPLIT_1W ? 4 : kWavesPerBlock;
+constexpr int kSplitTiles = DF_LDENSE_SPLIT_1W ? 4 : kLTiles;
 constexpr size_t kLdwLdsMax = 80 * 1024; // dW staging LDS (32 or 64 samples per step)
 #ifndef DF_LDW_DMA
 #define DF_LDW_DMA 1

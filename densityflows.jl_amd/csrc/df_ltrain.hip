@@ -30,23 +30,27 @@ __device__ __forceinline__ float gather_feature(const LDenseArgs& a, int slot, i
 // chunks (lane (g, i): A[16m + i, 32c + 16(e>>2) + 4g + (e&3)]), the B rows split on
 // the fly (df_uniform_impl.h), six products per chunk on bf16 MFMA onto the f32
 // accumulators (gradients: the 1e-4 criterion of the training tests).
-template <int MT, int IN, int EPI, bool SPLIT = false>
-__global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) {
+// NW waves of TT tiles each: the f32 instances 8 × kLTiles (two waves per SIMD); the SPLIT
+// ones kSplitWaves × kSplitTiles — one wave per SIMD whose 4 × 16 accumulator tiles sit
+// in the AGPR half of the register file, so every bf16x3 weight fragment read from LDS
+// feeds 4 tiles' products instead of 2 (same samples per workgroup round).
+template <int MT, int IN, int EPI, bool SPLIT = false, int NW = kWavesPerBlock, int TT = kLTiles>
+__global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int T = kLTiles;
+    constexpr int T = TT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, j = lane & 15;
     const int chunk_bytes = SPLIT ? MT * 3072 : a.chunk_kq * MT * 1024;
     const int nchunks = SPLIT ? a.nkq / 2 : (a.nkq + a.chunk_kq - 1) / a.chunk_kq;
     const int64_t ntiles = (a.batch + 15) / 16;
-    const int64_t per_round = (int64_t)gridDim.x * kWavesPerBlock * T;
+    const int64_t per_round = (int64_t)gridDim.x * NW * T;
     const int64_t rounds = (ntiles + per_round - 1) / per_round;
     const int64_t total = rounds * nchunks;
 
     auto dma = [&](int c, uint8_t* dst) {
         if constexpr (SPLIT) {
             const uint8_t* src = a.sfrag + (size_t)c * MT * 3072;
-            for (int q = wave; q < 3 * MT; q += kWavesPerBlock)
+            for (int q = wave; q < 3 * MT; q += NW)
                 __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (q << 10) + lane * 16),
                                                  (__attribute__((address_space(3))) void*)(dst + (q << 10)), 16, 0,
                                                  0);
@@ -56,7 +60,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
         const int kq1 = (kq0 + a.chunk_kq < a.nkq) ? kq0 + a.chunk_kq : a.nkq;
         const uint8_t* src = a.wfrag + (size_t)kq0 * MT * 1024;
         const int nk = (kq1 - kq0) * MT;  // KiB
-        for (int q = wave; q < nk; q += kWavesPerBlock)
+        for (int q = wave; q < nk; q += NW)
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (q << 10) + lane * 16),
                                              (__attribute__((address_space(3))) void*)(dst + (q << 10)), 16, 0,
                                              0);
@@ -67,7 +71,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
         // f32 fragments, or (SPLIT, a.w0s) bf16x3 planes [c][m][p][lane][8] of 32-row chunks
         const int n16 = (SPLIT && a.w0s) ? (a.w0t_nkq / 2) * a.w0t_mt * 3 * 64 : a.w0t_mt * a.w0t_nkq * 64;
         const f32x4* src = reinterpret_cast<const f32x4*>((SPLIT && a.w0s) ? a.w0s : a.w0t);
-        for (int q = threadIdx.x; q < n16; q += kBlockThreads) reinterpret_cast<f32x4*>(w0t_lds)[q] = src[q];
+        for (int q = threadIdx.x; q < n16; q += NW * 64) reinterpret_cast<f32x4*>(w0t_lds)[q] = src[q];
         // z̄ column of conditioner feature f (0xff: not an identity dim of z; d <= 64),
         // 64 bytes after the W0ᵀ fragments, fixed for the launch
         if (threadIdx.x < 64) {
@@ -84,7 +88,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
 
     int64_t i = 0;
     for (int64_t r = 0; r < rounds; ++r) {
-        const int64_t t0 = ((r * gridDim.x + blockIdx.x) * kWavesPerBlock + wave) * T;
+        const int64_t t0 = ((r * gridDim.x + blockIdx.x) * NW + wave) * T;
         int64_t smp[T];
         bool valid[T];
 #pragma unroll
@@ -119,7 +123,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1) ldense_kernel(LDenseArgs a) 
         // DACT epilogues: tile 0's first σ' arguments are loaded during the last k-quad
         // (the epilogues of all waves otherwise hit HBM in one burst)
         constexpr bool kDact = (EPI == LEPI_DACT || EPI == LEPI_DACT_XBAR);
-        constexpr int HR = MT < 8 ? MT : 8;  // σ' arguments in flight
+        constexpr int HR = (MT < 8 ? MT : 8) / (T > 2 ? 2 : 1);  // σ' arguments in flight
         const int64_t s0h = valid[0] ? smp[0] : a.batch - 1;
         f32x4 h0[kDact ? HR : 1];
         if constexpr (SPLIT && IN == LIN_BUF) {
@@ -697,7 +701,7 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
     for (int im = 0; im < 8; ++im)
 #pragma unroll
         for (int in = 0; in < 8; ++in) acc[im][in] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float dbp[4] = {0.f, 0.f, 0.f, 0.f};  // rows 4q + i, sample group sg
+    float dbp[4] = {0.f, 0.f, 0.f, 0.f};  // rows q + 64i, sample group sg
 
     // sample rows s = wave, wave + 4, .. of both operands (64 per step); a sample past
     // the workgroup's range is a row of zeros instead
@@ -716,16 +720,22 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
         }
     };
     // step 2 for one operand: rows 4q + i, samples 8sg + e
+    // Rows q + 64i (not 4q + i): the 16 lanes of a plane write then cover all 16
+    // (row & 3, slot) pairs, i.e. all 64 banks (rows 4 apart sit 256 B apart: one bank
+    // group per slot, 16-way).  The stage reads become dword reads of 64 consecutive
+    // floats (conflict-free).
     auto split_item = [&](int op, uint8_t* T, bool db) {
-        f32x4 x[8];
+        float x[4][8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = *reinterpret_cast<const f32x4*>(stage + (op * 32 + 8 * sg + e) * 256 + 4 * q);
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i][e] = stage[(op * 32 + 8 * sg + e) * 256 + q + 64 * i];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const float v[8] = {x[0][i], x[1][i], x[2][i], x[3][i], x[4][i], x[5][i], x[6][i], x[7][i]};
+            const float(&v)[8] = x[i];
             uni::bf16x8 p0, p1, p2;
             uni::split8(v, p0, p1, p2);
-            const int row = 4 * q + i;
+            const int row = q + 64 * i;
             uint8_t* dst = T + row * 64 + 16 * ldw_slot(row, sg);
             *reinterpret_cast<uni::bf16x8*>(dst) = p0;
             *reinterpret_cast<uni::bf16x8*>(dst + PB) = p1;
@@ -791,7 +801,7 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
     __syncthreads();
     float* dbl = lsm_f;  // [group][row]
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dbl[256 * sg + 4 * q + i] = dbp[i];
+    for (int i = 0; i < 4; ++i) dbl[256 * sg + q + 64 * i] = dbp[i];
     __syncthreads();
     if (a.b_off >= 0 && tid < a.m_true)
         dst[a.b_off + tid] = ((dbl[tid] + dbl[256 + tid]) + dbl[512 + tid]) + dbl[768 + tid];
@@ -991,8 +1001,10 @@ void* ldense_ptr_mt(int in_kind, int epi) {
 void* ldense_ptr(int mt, int in_kind, int epi, bool split = false) {
     if (split) {  // SPLIT instances: the W1ᵀδ1 products of hidden-256 conditioners
         if (mt != 16 || in_kind != LIN_BUF) return nullptr;
-        if (epi == LEPI_DACT) return reinterpret_cast<void*>(&ldense_kernel<16, LIN_BUF, LEPI_DACT, true>);
-        if (epi == LEPI_DACT_XBAR) return reinterpret_cast<void*>(&ldense_kernel<16, LIN_BUF, LEPI_DACT_XBAR, true>);
+        if (epi == LEPI_DACT)
+            return reinterpret_cast<void*>(&ldense_kernel<16, LIN_BUF, LEPI_DACT, true, kSplitWaves, kSplitTiles>);
+        if (epi == LEPI_DACT_XBAR)
+            return reinterpret_cast<void*>(&ldense_kernel<16, LIN_BUF, LEPI_DACT_XBAR, true, kSplitWaves, kSplitTiles>);
         return nullptr;
     }
     switch (mt) {
@@ -1014,7 +1026,7 @@ hipError_t launch_ldense(int mt, int in_kind, int epi, const LDenseArgs& a, unsi
     void* k = ldense_ptr(mt, in_kind, epi, a.sfrag != nullptr);
     if (!k) return hipErrorInvalidValue;
     void* args[] = {const_cast<LDenseArgs*>(&a)};
-    return hipLaunchKernel(k, dim3(grid), dim3(kBlockThreads), args, lds, st);
+    return hipLaunchKernel(k, dim3(grid), dim3(a.sfrag ? kSplitWaves * 64 : kBlockThreads), args, lds, st);
 }
 
 hipError_t ldense_occupancy(int mt, int in_kind, int epi, size_t lds, int* blocks) {
