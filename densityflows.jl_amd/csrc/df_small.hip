@@ -57,6 +57,23 @@ __device__ __forceinline__ T by_group(int g, T v0, T v1, T v2, T v3) {
     return g == 0 ? v0 : g == 1 ? v1 : g == 2 ? v2 : v3;
 }
 
+// The descriptor's first 128 dwords in two VGPRs (dword lane and 64 + lane), loaded with
+// the rows at kernel start; a layer's fields are then v_readlane's of them.  Read from the
+// kernel arguments instead, every field is a scalar load + wait inside the layer (the
+// compiler rematerialises them there rather than hold ~100 SGPRs), i.e. a scalar-cache
+// round trip per field per layer.
+struct DescRegs {
+    uint32_t v0, v1;
+    __device__ __forceinline__ uint32_t u32(int byte) const {
+        const int w = byte >> 2;
+        return (uint32_t)__builtin_amdgcn_readlane((int)(w < 64 ? v0 : v1), w & 63);
+    }
+    __device__ __forceinline__ int i8(int byte) const { return (int)(int8_t)(u32(byte) >> (8 * (byte & 3))); }
+    __device__ __forceinline__ float f32(int byte) const { return __uint_as_float(u32(byte)); }
+};
+#define SD_OFF(f) ((int)offsetof(SmallDesc, f))
+static_assert(offsetof(SmallDesc, norm_theta) <= 128 * 4, "DescRegs holds the first 128 dwords");
+
 // net k (0 = s, 1 = t) of layer li: its fragments at the blob offsets of the descriptor
 __device__ __forceinline__ void load_net(const ChainArgs& a, const SmallDesc& sd, int li, int k, NetW& w) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
@@ -139,6 +156,12 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
         const float v = *p;
         rv[q] = ((is_th || is_z) && valid) ? v : (c == nd + 3 ? 1.f : 0.f);
     }
+    DescRegs dr;
+    {
+        const uint32_t* sdw = reinterpret_cast<const uint32_t*>(&sd);
+        dr.v0 = sdw[lane];
+        dr.v1 = sdw[64 + lane];
+    }
     // every net's fragments (NormalizationLayers and NICE s-nets load the blob's first
     // bytes, never used: the loads stay one basic block)
     NetW ws[NL], wt[NL];
@@ -153,10 +176,11 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
         const int c = g + 4 * q;
         float v = rv[q];
         if (c < n && sd.norm_theta && valid) {  // normalize_input (Data.jl:213-218)
-            const float lo = q == 0 ? by_group(g, sd.tmin[0], sd.tmin[1], sd.tmin[2], sd.tmin[3])
-                                    : by_group(g, sd.tmin[4], sd.tmin[5], sd.tmin[6], sd.tmin[7]);
-            const float hi = q == 0 ? by_group(g, sd.tmax[0], sd.tmax[1], sd.tmax[2], sd.tmax[3])
-                                    : by_group(g, sd.tmax[4], sd.tmax[5], sd.tmax[6], sd.tmax[7]);
+            const int q4 = 4 * (q == 0 ? 0 : 1);
+            const float lo = by_group(g, dr.f32(SD_OFF(tmin) + 4 * q4), dr.f32(SD_OFF(tmin) + 4 * (q4 + 1)),
+                                      dr.f32(SD_OFF(tmin) + 4 * (q4 + 2)), dr.f32(SD_OFF(tmin) + 4 * (q4 + 3)));
+            const float hi = by_group(g, dr.f32(SD_OFF(tmax) + 4 * q4), dr.f32(SD_OFF(tmax) + 4 * (q4 + 1)),
+                                      dr.f32(SD_OFF(tmax) + 4 * (q4 + 2)), dr.f32(SD_OFF(tmax) + 4 * (q4 + 3)));
             const float diff = hi - lo;
             v = (diff == 0.f) ? 0.f : (v - lo) / diff;
         }
@@ -174,20 +198,20 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
 #pragma unroll
     for (int it = 0; it < NL; ++it) {
         const int li = FWD ? it : NL - 1 - it;
-        const int kind = sd.kind[li];
-        const bool first_in_elem = FWD ? sd.elem_start[li] : sd.elem_end[li];
-        const bool last_in_elem = FWD ? sd.elem_end[li] : sd.elem_start[li];
+        const int kind = dr.i8(SD_OFF(kind) + li);
+        const bool es = dr.i8(SD_OFF(elem_start) + li) != 0, ee = dr.i8(SD_OFF(elem_end) + li) != 0;
+        const bool first_in_elem = FWD ? es : ee;
+        const bool last_in_elem = FWD ? ee : es;
         if (kind == DF_LAYER_NORM) {  // src/norm/Normalization.jl:64-103
-            const float al = sd.alpha[li], be = sd.beta[li], delta = be - al;
+            const float al = dr.f32(SD_OFF(alpha) + 4 * li), be = dr.f32(SD_OFF(beta) + 4 * li), delta = be - al;
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const int i = g + 4 * q;
                 if (i < d) {
                     // lane group g's dims: the bounds by uniform index (register selects)
-                    const float lo = by_group(g, sd.xmin[li][4 * q], sd.xmin[li][4 * q + 1], sd.xmin[li][4 * q + 2],
-                                              sd.xmin[li][4 * q + 3]);
-                    const float hi = by_group(g, sd.xmax[li][4 * q], sd.xmax[li][4 * q + 1], sd.xmax[li][4 * q + 2],
-                                              sd.xmax[li][4 * q + 3]);
+                    const int x0 = SD_OFF(xmin) + 4 * (8 * li + 4 * q), x1 = SD_OFF(xmax) + 4 * (8 * li + 4 * q);
+                    const float lo = by_group(g, dr.f32(x0), dr.f32(x0 + 4), dr.f32(x0 + 8), dr.f32(x0 + 12));
+                    const float hi = by_group(g, dr.f32(x1), dr.f32(x1 + 4), dr.f32(x1 + 8), dr.f32(x1 + 12));
                     const float xd = hi - lo;
                     float v = row[n + i];
                     if (FWD) v = ((xd * v - al * hi) + be * lo) / delta;
@@ -195,12 +219,14 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
                     row[n + i] = v;
                 }
             }
-            ldj_update(FWD ? sd.ldj_const[li] : -sd.ldj_const[li], first_in_elem, last_in_elem);
+            const float lc = dr.f32(SD_OFF(ldj_const) + 4 * li);
+            ldj_update(FWD ? lc : -lc, first_in_elem, last_in_elem);
         } else {
             const bool rnvp = (kind == DF_LAYER_RNVP);
-            const int fslot = by_group<int>(g, sd.feat[li][0], sd.feat[li][1], sd.feat[li][2], sd.feat[li][3]);
+            // byte g of the layer's feature / transformed-dim words (slots < 13: unsigned)
+            const int fslot = (int)((dr.u32(SD_OFF(feat) + 4 * li) >> (8 * g)) & 0xffu);
             const float xin = row[fslot];
-            const int slot = by_group<int>(g, sd.af[li][0], sd.af[li][1], sd.af[li][2], sd.af[li][3]);
+            const int slot = (int)((dr.u32(SD_OFF(af) + 4 * li) >> (8 * g)) & 0xffu);
             auto couple = [&](auto no_tag) {
                 constexpr int NO = decltype(no_tag)::value;
                 const float ys = rnvp ? eval_net<NO>(ws[li], xin) : 0.f;
@@ -220,7 +246,7 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
                 const float sum = rnvp ? uni::group_row_sum<NO>(ys) : 0.f;
                 ldj_update(rnvp ? (FWD ? sum : -sum) : 0.f, first_in_elem, last_in_elem);
             };
-            switch (sd.n_out[li]) {
+            switch (dr.i8(SD_OFF(n_out) + li)) {
                 case 1: couple(std::integral_constant<int, 1>{}); break;
                 case 2: couple(std::integral_constant<int, 2>{}); break;
                 case 3: couple(std::integral_constant<int, 3>{}); break;

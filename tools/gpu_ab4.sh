@@ -22,6 +22,7 @@ for rep in $(seq 1 ${REPS:-2}); do
       case $w in
         cfg5) run cfg5 $lib $rep "--mode train --config cfg4 --steps 5 --warmup 2" || exit 1 ;;
         cfg1) run cfg1 $lib $rep "--config cfg1 --steps 300 --warmup 50" || exit 1 ;;
+        cfg1s) run cfg1s $lib $rep "--config cfg1 --batch 4096 --steps 300 --warmup 50" || exit 1 ;;
         cfg2) run cfg2 $lib $rep "--steps 200 --warmup 50 --no-exact" || exit 1 ;;
         train2) run train2 $lib $rep "--mode train --steps 20 --warmup 5" || exit 1 ;;
         cfg4) run cfg4 $lib $rep "--config cfg4 --steps 10 --warmup 3 --no-exact" || exit 1 ;;
@@ -29,6 +30,14 @@ for rep in $(seq 1 ${REPS:-2}); do
     done
   done
 done
+if [ -n "${PROF:-}" ]; then  # kernel trace of the in-tree build on config 1 at B = 4096
+  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof -o cfg1s -- \
+      python3 $GRAFT_REPO_ROOT/bench.py --config cfg1 --batch 4096 --steps 300 --warmup 50 --no-cpu --no-clock \
+      > $GRAFT_REPO_ROOT/$O/prof_cfg1s.json 2> $GRAFT_REPO_ROOT/$O/prof_cfg1s.err || exit 1
+  cd $GRAFT_REPO_ROOT
+  python3 tools/kgap.py $(find $O/prof -name "*kernel_trace.csv" | head -1) > $O/kgap_cfg1s.txt || exit 1
+  cat $O/kgap_cfg1s.txt
+fi
 for f in $O/*_lib*.json; do
   python3 -c "
 import json
