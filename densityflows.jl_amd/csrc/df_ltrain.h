@@ -33,7 +33,7 @@ constexpr int kLChunkBytes = 32 * 1024;  // weight chunk (LDS, double-buffered)
 #endif
 constexpr int kLTiles = DF_LTILES;       // 16-sample tiles per wave per round
 #ifndef DF_LDENSE_SPLIT_1W
-#define DF_LDENSE_SPLIT_1W 1
+#define DF_LDENSE_SPLIT_1W 0
 #endif
 // SPLIT (hidden-256 W1ᵀδ1) instances: waves per workgroup × tiles per wave (samples per
 // workgroup round = kWavesPerBlock · kLTiles either way)
@@ -106,15 +106,6 @@ struct LdwArgs {
     int w_off, b_off;       // trainables offsets (b_off -1: no bias)
     int64_t batch;
     int split;              // 1: bf16x3 split products (ldw_split_kernel, its own launch; mta = ntb = 16)
-    // g_feat != nullptr: the B operand is the conditioner input vcat(θ, u)[axis_nn] gathered
-    // on the fly (dW0 of a net whose hidden activations the inverse pass kept: no separate
-    // gather launch and no [B][ld] copy); rows >= g_nin are zero
-    const int32_t* g_feat;
-    const float* g_theta;
-    const float* g_tmin;
-    const float* g_tmax;
-    const float* g_u;
-    int g_nin, g_n, g_d;
 };
 
 // One merged launch: up to three non-split dW products (ldw) of net i and, optionally, the

@@ -583,31 +583,7 @@ __device__ __forceinline__ void ldw_body(const LdwArgs& a, float* lsm, int bid, 
             }
             if (e < nb) {
                 const int ss = e / qb, rq = e - ss * qb;
-                if (s0 + ss < s_end) {
-                    if (a.g_feat) {  // gather_feature (normalize_input for θ, Data.jl:213-218)
-                        const int64_t smp = s0 + ss;
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const int f = 4 * rq + q;
-                            float v = 0.f;
-                            if (f < a.g_nin) {
-                                const int slot = a.g_feat[f];
-                                if (slot < a.g_n) {
-                                    v = a.g_theta[smp * a.g_n + slot];
-                                    if (a.g_tmin) {
-                                        const float lo = a.g_tmin[slot], diff = a.g_tmax[slot] - lo;
-                                        v = (diff == 0.f) ? 0.f : (v - lo) / diff;
-                                    }
-                                } else if (slot < a.g_n + a.g_d) {
-                                    v = a.g_u[smp * a.g_d + (slot - a.g_n)];
-                                }
-                            }
-                            pb[k][q] = v;
-                        }
-                    } else {
-                        pb[k] = *reinterpret_cast<const f32x4*>(a.xb + (s0 + ss) * a.ldb + 4 * rq);
-                    }
-                }
+                if (s0 + ss < s_end) pb[k] = *reinterpret_cast<const f32x4*>(a.xb + (s0 + ss) * a.ldb + 4 * rq);
             }
         }
     };

@@ -592,13 +592,6 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
     const bool no_fuse = std::getenv("DF_TRAIN_NOFUSE") && std::getenv("DF_TRAIN_NOFUSE")[0] == '1';
     const bool no_merge = std::getenv("DF_TRAIN_NOMERGE") && std::getenv("DF_TRAIN_NOMERGE")[0] == '1';
     auto keeps = [&](const SweepOp& op) { return t->hsave_on && !t->lnets[op.net].pre; };
-    // the inverse pass kept the hidden activations and the first Dense is not the net's
-    // only one: its input is needed by dW0 alone, which gathers it itself (DF_TRAIN_GATHER=1:
-    // the separate gather launch into d_lx, the round-3 form)
-    const bool sep_gather = std::getenv("DF_TRAIN_GATHER") && std::getenv("DF_TRAIN_GATHER")[0] == '1';
-    auto gather_in_dw = [&](const SweepOp& op) {
-        return keeps(op) && t->lnets[op.net].dn.size() > 1 && !sep_gather;
-    };
     auto fused_front = [&](const SweepOp& op) {
         const LNet& N = t->lnets[op.net];
         const int nd = (int)N.dn.size();
@@ -647,17 +640,6 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             w.m_true = D.out_dim;
             w.mta = D.fwd.mt;
             w.xb = (k == 0) ? t->d_lx : Hbuf(op, k - 1);
-            if (k == 0 && gather_in_dw(op)) {  // dW0 gathers its B operand itself
-                const LDenseArgs b = base_args(op);
-                w.g_feat = b.feat;
-                w.g_theta = b.theta;
-                w.g_tmin = b.tmin;
-                w.g_tmax = b.tmax;
-                w.g_u = b.u_in;
-                w.g_nin = b.n_in;
-                w.g_n = b.n;
-                w.g_d = b.d;
-            }
             w.ldb = W;
             w.n_true = D.in_dim;
             w.ntb = D.bwd.mt;
@@ -701,7 +683,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             LDenseArgs a = b;
             a.act = N.dn[k].act;
             if (k + 1 < nd && keep) {
-                if (k == 0 && !gather_in_dw(op)) {
+                if (k == 0) {
                     a.xsave = t->d_lx;
                     e = e == hipSuccess ? launch_gather_features(a, 16 * N.dn[0].bwd.mt, st) : e;
                 }

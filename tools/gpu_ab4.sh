@@ -19,7 +19,7 @@ run() {  # <name> <lib> <rep> <bench args>   (lib "env": the in-tree build under
       > $O/$1_${tag}_$3.json 2> $O/$1_${tag}_$3.err
 }
 for rep in $(seq 1 ${REPS:-2}); do
-  for lib in libdf_old.so libdensityflows_hip.so ${ABENV:+env}; do
+  for lib in ${LIBS:-libdf_old.so libdensityflows_hip.so} ${ABENV:+env}; do
     for w in ${AB:-cfg5 cfg1}; do
       case $w in
         cfg5) run cfg5 $lib $rep "--mode train --config cfg4 --steps 5 --warmup 2" || exit 1 ;;
@@ -33,14 +33,14 @@ for rep in $(seq 1 ${REPS:-2}); do
   done
 done
 if [ -n "${PROF:-}" ]; then  # kernel trace of the in-tree build on config 1 at B = 4096
-  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$O/prof -o cfg1s -- \
+  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o cfg1s -- \
       python3 $GRAFT_REPO_ROOT/bench.py --config cfg1 --batch 4096 --steps 300 --warmup 50 --no-cpu --no-clock \
       > $GRAFT_REPO_ROOT/$O/prof_cfg1s.json 2> $GRAFT_REPO_ROOT/$O/prof_cfg1s.err || exit 1
   cd $GRAFT_REPO_ROOT
   python3 tools/kgap.py $(find $O/prof -name "*kernel_trace.csv" | head -1) > $O/kgap_cfg1s.txt || exit 1
   cat $O/kgap_cfg1s.txt
 fi
-for f in $O/*_lib*.json $O/*_env_*.json; do
+for f in $O/*_lib*.json $O/*_env_*.json $O/*_env.json; do
   [ -f "$f" ] || continue
   python3 -c "
 import json
