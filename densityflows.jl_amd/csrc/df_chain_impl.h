@@ -120,9 +120,20 @@ struct Stager {
     __device__ __forceinline__ uint8_t* buf() const { return base + ((idx & 1) ? bytes : 0); }
 };
 
+// Stage descriptors and schedules are read through the constant address space (scalar
+// loads: the host writes them before the launch, nothing in a kernel stores to them) and
+// the wave index is made scalar: read as generic pointers they were vector loads, each
+// followed by a vmcnt(0) wait, and the source address a VGPR pair (spilled in the
+// FAST SPLIT kernel, whose reload's vmcnt(0) then also waited for the DMA just issued).
+template <typename T>
+__device__ __forceinline__ T cload(const T* p, int64_t i) {
+    using CT = const __attribute__((address_space(4))) T;
+    return *(const T*)(&((CT*)(uintptr_t)p)[i]);
+}
+
 __device__ __forceinline__ void dma_stage(const ChainArgs& a, int s, uint8_t* dst) {
-    const DevStage st = a.stages[s];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const DevStage st = cload(a.stages, s);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint8_t* src = a.blob + st.src_off;
     const int nchunk = st.bytes >> 10;
     for (int c = wave; c < nchunk; c += kWavesPerBlock) {
@@ -135,7 +146,7 @@ __device__ __forceinline__ void dma_stage(const ChainArgs& a, int s, uint8_t* ds
 __device__ __forceinline__ void stager_start(Stager& sg, const ChainArgs& a) {
     sg.idx = -1;
     sg.cur = -1;
-    if (sg.n > 0) dma_stage(a, sg.sched[0], sg.base);
+    if (sg.n > 0) dma_stage(a, cload(sg.sched, 0), sg.base);
 }
 
 // Make stage `s` resident (uniform across the workgroup).
@@ -149,9 +160,9 @@ __device__ __forceinline__ void ensure_stage(int s, Stager& sg, const ChainArgs&
     __syncthreads();                                     // ... every wave's, and buffer (nidx+1)&1 is free
     sg.idx = nidx;
     sg.cur = s;
-    if (nidx >= sg.n || sg.sched[nidx] != s) {
+    if (nidx >= sg.n || cload(sg.sched, nidx) != s) {
         // off-schedule request (not produced by the planner): synchronous copy
-        const DevStage st = a.stages[s];
+        const DevStage st = cload(a.stages, s);
         const f32x4* src = reinterpret_cast<const f32x4*>(a.blob + st.src_off);
         f32x4* dst = reinterpret_cast<f32x4*>(sg.buf());
         for (int i = threadIdx.x; i < (st.bytes >> 4); i += kBlockThreads) dst[i] = src[i];
@@ -159,7 +170,7 @@ __device__ __forceinline__ void ensure_stage(int s, Stager& sg, const ChainArgs&
         sg.n = 0;  // schedule abandoned: every further switch copies synchronously
         return;
     }
-    if (nidx + 1 < sg.n) dma_stage(a, sg.sched[nidx + 1], sg.base + (((nidx + 1) & 1) ? sg.bytes : 0));
+    if (nidx + 1 < sg.n) dma_stage(a, cload(sg.sched, nidx + 1), sg.base + (((nidx + 1) & 1) ? sg.bytes : 0));
 }
 
 constexpr int out_tiles(int HT) { return HT < 2 ? HT : 2; }
