@@ -863,13 +863,15 @@ uniform_kernel(ChainArgs a) {
                 for (int tt = 0; tt < nt; tt += kTT) {
                     int ro[kTT];
                     float ssum[kTT];
-                    // the row offsets from one opaque copy of row0 per tile group: left to
-                    // itself the compiler strength-reduces every state address of the loop
-                    // into its own VGPR induction variable (six), which the SPLIT kernel at
-                    // 128 VGPRs spills — and a reload's vmcnt(0) also waits for the stage
-                    // DMA issued just before
+                    // SPLIT: the row offsets from one opaque copy of row0 per tile group:
+                    // left to itself the compiler strength-reduces every state address of
+                    // the loop into its own VGPR induction variable (six), which the SPLIT
+                    // kernel at 128 VGPRs spills — and a reload's vmcnt(0) also waits for the
+                    // stage DMA issued just before (headline 1583 -> 1623 Msamples/s,
+                    // gpurun_out/ab4e; the exact-f32 kernels keep the induction variables:
+                    // config 1 at 2^20 lost 0.9% with the opaque copy)
                     int r0 = row0;
-                    asm volatile("" : "+v"(r0));
+                    if constexpr (SPLIT) asm volatile("" : "+v"(r0));
 #pragma unroll
                     for (int t = 0; t < kTT; ++t) ro[t] = r0 + (tt + t) * tstep;
                     net_tiles<HT, kTT, OUTV, RELU, PH, FAST, NO, SPLIT>(buf, N, L, tab, state, ro, ssum);
