@@ -201,6 +201,7 @@ int df_chain_create(df_chain** out, const df_chain_desc* desc, int device) {
     c->debug_launch = std::getenv("DF_DEBUG_LAUNCH") && std::getenv("DF_DEBUG_LAUNCH")[0] == '1';
     if (const char* e = std::getenv("DF_TILES")) c->force_tiles = std::atoi(e);
     if (const char* e = std::getenv("DF_SMALL_MAX")) c->small_max = std::max<int64_t>(0, std::atoll(e));
+    if (const char* e = std::getenv("DF_SMALL_WAVES")) c->small_waves = std::atoi(e) == 1 ? 1 : 2;
     int rc = df::build_plan(desc, &c->plan, &err, c->exact ? 1 : 0);
     if (rc != DF_OK) {
         delete c;
@@ -580,7 +581,7 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
             c->small_sd[fi] = small_desc(c, flow);
             c->small_sd_ok[fi] = true;
         }
-        e = df::launch_small(mode, a, c->small_sd[fi], (unsigned)grid, st);
+        e = df::launch_small(mode, a, c->small_sd[fi], (unsigned)grid, st, c->small_waves);
     } else if (split) {
         a.blob = static_cast<const uint8_t*>(c->d_sblob);
         a.stages = static_cast<const df::DevStage*>(c->d_sstages);

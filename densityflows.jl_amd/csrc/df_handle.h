@@ -22,6 +22,7 @@ struct df_chain {
     bool debug_launch = false;
     int force_tiles = 0;
     int64_t small_max = -1;
+    int small_waves = 2;  // DF_SMALL_WAVES: waves per small-kernel workgroup (1 or 2)
     // the small-batch kernel's descriptor, by flow (θ normalised) 0 / 1; rebuilt after
     // df_chain_set_weights / df_chain_set_theta_bounds
     df::SmallDesc small_sd[2] = {};

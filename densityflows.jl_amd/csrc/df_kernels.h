@@ -123,6 +123,8 @@ struct SmallDesc {
     float tmin[8], tmax[8];                              // θ bounds (n <= 8)
     int32_t norm_theta;                                  // θ raw: normalise it with tmin / tmax
 };
-hipError_t launch_small(int mode, const ChainArgs& a, const SmallDesc& sd, unsigned grid, hipStream_t st);
+// nw = 2 (default): the s- and t-nets of a layer on two waves of the workgroup; 1: one wave
+hipError_t launch_small(int mode, const ChainArgs& a, const SmallDesc& sd, unsigned grid, hipStream_t st,
+                        int nw = 2);
 
 }  // namespace df

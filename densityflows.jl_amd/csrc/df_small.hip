@@ -123,16 +123,28 @@ __device__ __forceinline__ float eval_net(const NetW& w, float xin) {
     return (__uint_as_float(c[0]) + __uint_as_float(c[1])) + w.bo;
 }
 
-template <int MODE, int NL>
-__global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd) {
+// NW = 2: the s-net of every layer on wave 0 and the t-net on wave 1 of the workgroup
+// (the two nets of a layer read the same features, RNVP.jl:174-177, and are
+// independent).  Wave 1 hands its outputs over in LDS; wave 0 applies the coupling and
+// keeps the ldj; a barrier after each layer gives wave 1 the updated row.  Both waves
+// write the initial row (identical values), so the first layer needs no barrier.
+// Each wave issues one net's instructions per layer instead of two.
+// The barriers are bare (lgkmcnt(0) + s_barrier): the LDS row and the handed-over
+// outputs are the only data the waves share; no global load needs to land for them.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int MODE, int NL, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) small_kernel(ChainArgs a, SmallDesc sd) {
     constexpr bool FWD = (MODE == MODE_FWD || MODE == MODE_FWD_INPLACE);
     constexpr bool WANT_LDJ = (MODE != MODE_FWD_INPLACE);
     __shared__ float srow[16 * kStride];
+    __shared__ float yx[NW == 2 ? 64 : 1];  // NW = 2: wave 1's t-net outputs, by lane
+    const int wv = NW == 2 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
     ClockStamp clk;
     clk.begin(a);
 #ifdef DF_PHASE_STAMPS  // diagnostic build (wrong outputs): wave 0 of workgroup 0 stamps its phases
     uint64_t ph[12] = {};
-#define DF_PH(i) do { if (blockIdx.x == 0) ph[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#define DF_PH(i) do { if (blockIdx.x == 0 && wv == 0) ph[i] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define DF_PH(i) do {} while (0)
 #endif
@@ -164,11 +176,11 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
     }
     // every net's fragments (NormalizationLayers and NICE s-nets load the blob's first
     // bytes, never used: the loads stay one basic block)
-    NetW ws[NL], wt[NL];
+    NetW ws[NL], wt[NW == 1 ? NL : 1];  // NW = 2: ws holds this wave's net (s: wave 0, t: wave 1)
 #pragma unroll
     for (int li = 0; li < NL; ++li) {
-        load_net(a, sd, li, 0, ws[li]);
-        load_net(a, sd, li, 1, wt[li]);
+        load_net(a, sd, li, NW == 1 ? 0 : wv, ws[li]);
+        if constexpr (NW == 1) load_net(a, sd, li, 1, wt[li]);
     }
 
 #pragma unroll
@@ -216,7 +228,7 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
                     float v = row[n + i];
                     if (FWD) v = ((xd * v - al * hi) + be * lo) / delta;
                     else v = (be * (v - lo) + al * (hi - v)) / xd;
-                    row[n + i] = v;
+                    if (wv == 0) row[n + i] = v;
                 }
             }
             const float lc = dr.f32(SD_OFF(ldj_const) + 4 * li);
@@ -229,8 +241,18 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
             const int slot = (int)((dr.u32(SD_OFF(af) + 4 * li) >> (8 * g)) & 0xffu);
             auto couple = [&](auto no_tag) {
                 constexpr int NO = decltype(no_tag)::value;
-                const float ys = rnvp ? eval_net<NO>(ws[li], xin) : 0.f;
-                const float yt = eval_net<NO>(wt[li], xin);
+                float ys, yt;
+                if constexpr (NW == 1) {
+                    ys = rnvp ? eval_net<NO>(ws[li], xin) : 0.f;
+                    yt = eval_net<NO>(wt[li], xin);
+                } else {
+                    const float y = (wv == 1 || rnvp) ? eval_net<NO>(ws[li], xin) : 0.f;
+                    if (wv == 1) yx[lane] = y;
+                    lds_barrier();
+                    if (wv == 1) return;
+                    ys = y;
+                    yt = yx[lane];
+                }
                 if (g < NO) {
                     float v = row[slot];
                     if (FWD) {
@@ -255,7 +277,10 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
         }
         have_acc = have_acc || last_in_elem;
         DF_PH(2 + it);
-        if (!FWD && a.snap && valid) {  // training: every layer's output for the reverse sweep
+        if constexpr (NW == 2) {
+            lds_barrier();  // wave 0's row update → wave 1's next features
+        }
+        if (!FWD && a.snap && valid && wv == 0) {  // training: every layer's output for the reverse sweep
             float* dst = a.snap + (int64_t)li * a.batch * d;
 #pragma unroll
             for (int q = 0; q < 2; ++q)
@@ -263,6 +288,7 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
         }
     }
 
+    if (NW == 2 && wv == 1) return;  // wave 0 holds the ldj and writes every output
     if (MODE == MODE_LOGPDF) {
         double part = 0.0;
         if (g == 0) {
@@ -306,33 +332,37 @@ __global__ void __launch_bounds__(64, 1) small_kernel(ChainArgs a, SmallDesc sd)
     clk.end(a);
 }
 
-template <int MODE>
+template <int MODE, int NW>
 void* kernel_ptr_m(int nl) {
     switch (nl) {
-        case 1: return reinterpret_cast<void*>(&small_kernel<MODE, 1>);
-        case 2: return reinterpret_cast<void*>(&small_kernel<MODE, 2>);
-        case 3: return reinterpret_cast<void*>(&small_kernel<MODE, 3>);
-        case 4: return reinterpret_cast<void*>(&small_kernel<MODE, 4>);
+        case 1: return reinterpret_cast<void*>(&small_kernel<MODE, 1, NW>);
+        case 2: return reinterpret_cast<void*>(&small_kernel<MODE, 2, NW>);
+        case 3: return reinterpret_cast<void*>(&small_kernel<MODE, 3, NW>);
+        case 4: return reinterpret_cast<void*>(&small_kernel<MODE, 4, NW>);
         default: return nullptr;
     }
 }
 
-void* kernel_ptr(int mode, int nl) {
+template <int NW>
+void* kernel_ptr_w(int mode, int nl) {
     switch (mode) {
-        case MODE_FWD: return kernel_ptr_m<MODE_FWD>(nl);
-        case MODE_FWD_INPLACE: return kernel_ptr_m<MODE_FWD_INPLACE>(nl);
-        case MODE_BWD: return kernel_ptr_m<MODE_BWD>(nl);
-        default: return kernel_ptr_m<MODE_LOGPDF>(nl);
+        case MODE_FWD: return kernel_ptr_m<MODE_FWD, NW>(nl);
+        case MODE_FWD_INPLACE: return kernel_ptr_m<MODE_FWD_INPLACE, NW>(nl);
+        case MODE_BWD: return kernel_ptr_m<MODE_BWD, NW>(nl);
+        default: return kernel_ptr_m<MODE_LOGPDF, NW>(nl);
     }
 }
 
+void* kernel_ptr(int mode, int nl, int nw) { return nw == 2 ? kernel_ptr_w<2>(mode, nl) : kernel_ptr_w<1>(mode, nl); }
+
 }  // namespace small
 
-hipError_t launch_small(int mode, const ChainArgs& a, const SmallDesc& sd, unsigned grid, hipStream_t st) {
-    void* f = small::kernel_ptr(mode, a.n_layers);
+hipError_t launch_small(int mode, const ChainArgs& a, const SmallDesc& sd, unsigned grid, hipStream_t st, int nw) {
+    nw = nw == 1 ? 1 : 2;
+    void* f = small::kernel_ptr(mode, a.n_layers, nw);
     if (!f) return hipErrorInvalidValue;
     void* args[] = {const_cast<ChainArgs*>(&a), const_cast<SmallDesc*>(&sd)};
-    return hipLaunchKernel(f, dim3(grid), dim3(64), args, 0, st);
+    return hipLaunchKernel(f, dim3(grid), dim3(64 * nw), args, 0, st);
 }
 
 }  // namespace df

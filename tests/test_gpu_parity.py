@@ -650,7 +650,8 @@ def test_small_kernel_bitwise_fast_kernel(cuda, B, monkeypatch, capfd):
     from the blob, no LDS) against the FAST kernel it replaces at small batches
     (DF_SMALL_MAX=0): forward, forward!, inverse, per-sample logpdf and the inverse
     pass's per-layer outputs (training snapshots, via a gradient) bitwise; the
-    fp64 Σ logpdf to rounding of its summation order."""
+    fp64 Σ logpdf to rounding of its summation order.  Both forms of the small kernel:
+    the s- and t-nets of a layer on two waves (default) and on one (DF_SMALL_WAVES=1)."""
     import torch
 
     from densityflows_amd.train import Adam, HIPTrainer
@@ -660,10 +661,13 @@ def test_small_kernel_bitwise_fast_kernel(cuda, B, monkeypatch, capfd):
         np.random.default_rng(B).standard_normal((5, B)).astype(np.float32)
     th = np.random.default_rng(B + 1).uniform(-1, 2, (1, B)).astype(np.float32)
     res = {}
-    for mode in ("small", "fast"):
+    for mode in ("small", "small1", "fast"):
         monkeypatch.delenv("DF_SMALL_MAX", raising=False)
+        monkeypatch.delenv("DF_SMALL_WAVES", raising=False)
         if mode == "fast":
             monkeypatch.setenv("DF_SMALL_MAX", "0")
+        if mode == "small1":
+            monkeypatch.setenv("DF_SMALL_WAVES", "1")
         monkeypatch.setenv("DF_DEBUG_LAUNCH", "1")
         chain = spec_to_element(spec)
         flow = dfa.Flow(chain, metadata=dfa.MetaData("", 5, 1, g["theta_min"], g["theta_max"]))
@@ -679,13 +683,14 @@ def test_small_kernel_bitwise_fast_kernel(cuda, B, monkeypatch, capfd):
         tr.gradient(xflat, _t(th, cuda).T.contiguous().reshape(-1), B, B, lps)
         torch.cuda.synchronize()
         launches = capfd.readouterr().err
-        assert ("kernel small " in launches) == (mode == "small"), launches
+        assert ("kernel small " in launches) == (mode != "fast"), launches
         res[mode] = ([_np(v) for v in (x, lf, zb, lb, zz, lp)], float(s.item()), tr.grad().cpu().numpy().copy(),
                      float(lps.item()))
         monkeypatch.delenv("DF_DEBUG_LAUNCH", raising=False)
-    for a, b in zip(res["small"][0], res["fast"][0]):
-        np.testing.assert_array_equal(a, b)
-    np.testing.assert_allclose(res["small"][1], res["fast"][1], rtol=1e-12, atol=1e-9)
-    np.testing.assert_allclose(res["small"][3], res["fast"][3], rtol=1e-12, atol=1e-9)
-    # the gradient reads the inverse pass's snapshots: equal snapshots → equal gradient
-    np.testing.assert_array_equal(res["small"][2], res["fast"][2])
+    for m in ("small", "small1"):
+        for a, b in zip(res[m][0], res["fast"][0]):
+            np.testing.assert_array_equal(a, b)
+        np.testing.assert_allclose(res[m][1], res["fast"][1], rtol=1e-12, atol=1e-9)
+        np.testing.assert_allclose(res[m][3], res["fast"][3], rtol=1e-12, atol=1e-9)
+        # the gradient reads the inverse pass's snapshots: equal snapshots → equal gradient
+        np.testing.assert_array_equal(res[m][2], res["fast"][2])
