@@ -15,11 +15,12 @@ fi
 run() {  # <name> <lib> <rep> <bench args>   (lib "env": the in-tree build under $ABENV)
   local so=$2 tag=${2%.so} envs=""
   if [ "$2" = env ]; then so=libdensityflows_hip.so; envs="$ABENV"; fi
+  if [ "$2" = env2 ]; then so=libdensityflows_hip.so; envs="$ABENV2"; fi
   env $envs DENSITYFLOWS_HIP_LIB=densityflows.jl_amd/$so timeout -k 10 300 python3 bench.py $4 --no-cpu \
       > $O/$1_${tag}_$3.json 2> $O/$1_${tag}_$3.err
 }
 for rep in $(seq 1 ${REPS:-2}); do
-  for lib in ${LIBS:-libdf_old.so libdensityflows_hip.so} ${ABENV:+env}; do
+  for lib in ${LIBS:-libdf_old.so libdensityflows_hip.so} ${ABENV:+env} ${ABENV2:+env2}; do
     for w in ${AB:-cfg5 cfg1}; do
       case $w in
         cfg5) run cfg5 $lib $rep "--mode train --config cfg4 --steps 5 --warmup 2" || exit 1 ;;
@@ -40,7 +41,7 @@ if [ -n "${PROF:-}" ]; then  # kernel trace of the in-tree build on config 1 at 
   python3 tools/kgap.py $(find $O/prof -name "*kernel_trace.csv" | head -1) > $O/kgap_cfg1s.txt || exit 1
   cat $O/kgap_cfg1s.txt
 fi
-for f in $O/*_lib*.json $O/*_env_*.json $O/*_env.json; do
+for f in $O/*_lib*.json $O/*_env_*.json $O/*_env2_*.json; do
   [ -f "$f" ] || continue
   python3 -c "
 import json
