@@ -175,10 +175,14 @@ def _fast_case_chain(case, rng):
                                    L(dfa.NICECouplingLayer, 5, [5, 1, 2], n=1, hidden_dim=32, rng=rng))
     if case == "block_h16":    # CouplingBlocks, hidden 16
         return 5, 0, dfa.FlowChain.repeat(dfa.CouplingBlock, 2, 5, hidden_dim_s=16, hidden_dim_t=16, rng=rng)
+    if case == "nice_h16":     # NICE + RNVP, conditioned, hidden 16: the small kernel's NICE layers
+        return 5, 1, dfa.FlowChain(L(dfa.NICECouplingLayer, 5, [1, 2, 3], n=1, hidden_dim=16, rng=rng),
+                                   L(5, [3, 4, 5], n=1, hidden_dim=16, rng=rng),
+                                   L(dfa.NICECouplingLayer, 5, [5, 1, 2], n=1, hidden_dim=16, rng=rng))
     raise ValueError(case)
 
 
-@pytest.mark.parametrize("case", ["af1_h64", "af4_h64", "in4_h64", "nice_h32", "block_h16"])
+@pytest.mark.parametrize("case", ["af1_h64", "af4_h64", "in4_h64", "nice_h32", "block_h16", "nice_h16"])
 def test_fast_variant_cases(cuda, case, monkeypatch, capfd):
     """FAST-variant tails for every output count: against the fp64 oracle, and
     bitwise against the non-FAST / unfolded plans of the same chain; the small-batch
@@ -207,7 +211,7 @@ def test_fast_variant_cases(cuda, case, monkeypatch, capfd):
         zb, lb = dfa.backward(chain, x, tth)
         if "SPLIT" in env:   # the bf16x3 SPLIT kernel (hidden 32 / 64): f32-accurate, not bitwise
             assert _kernel_of(chain) in ((4,) if case in ("af1_h64", "af4_h64", "nice_h32") else
-                                         (3,) if case == "block_h16" else (1, 2))
+                                         (3,) if case in ("block_h16", "nice_h16") else (1, 2))
             xo, lo = O.forward(chain.to_spec(), z, th if n else np.zeros((0, B), np.float32), np.float64)
             assert close(_np(x), xo, RTOL)[0] and close(_np(lf), lo, RTOL)[0]
             assert np.all(np.abs(_np(lf) + _np(lb)) <= 2e-6 + 1e-5 * np.abs(_np(lf)))
@@ -220,7 +224,7 @@ def test_fast_variant_cases(cuda, case, monkeypatch, capfd):
             launches = capfd.readouterr().err
             # hidden-16 FAST chains of <= 4 layers at this batch run the small-batch kernel (df_small.hip),
             # whose outputs are bitwise the FAST kernel's (the comparisons below)
-            small = case == "block_h16" and "DF_SMALL_MAX" not in env
+            small = case in ("block_h16", "nice_h16") and "DF_SMALL_MAX" not in env
             want = ("kernel uniform " if case == "in4_h64" else "kernel small " if small else
                     "kernel uniform-fast ")
             assert want in launches, launches
