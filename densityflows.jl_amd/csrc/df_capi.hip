@@ -86,11 +86,7 @@ static df::SmallDesc small_desc(const df_chain* c, bool flow) {
             sd.wo[li][k] = (int32_t)(base + nets[k]->off_out);
         }
     }
-    sd.norm_theta = (flow && P.n > 0) ? 1 : 0;
-    for (int i = 0; sd.norm_theta && i < P.n && i < 8; ++i) {
-        sd.tmin[i] = c->h_bounds[i];
-        sd.tmax[i] = c->h_bounds[P.n + i];
-    }
+    (void)flow;
     return sd;
 }
 
@@ -467,7 +463,8 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     const bool wide = P.wide && !c->no_wide;
     const bool split = !wide && use_split(c);
     const bool small = !wide && !split && use_small(c, batch);
-    const int tiles = wide ? df::kWideT : small ? 2 : choose_tiles(c, mode, batch, split);
+    // (the small kernel runs one 16-sample tile per workgroup: tiles = 1, only reported)
+    const int tiles = wide ? df::kWideT : small ? 1 : choose_tiles(c, mode, batch, split);
     {
         if (c->debug_launch) {  // tuning aid (DF_DEBUG_LAUNCH=1): the launch shape on stderr
             std::fprintf(stderr, "[df] mode %d batch %lld kernel %s tiles %d (max %d) occupancy:", mode,

@@ -120,8 +120,8 @@ struct SmallDesc {
     int8_t af[kSmallLayers][4];    // state columns of the transformed dims
     float alpha[kSmallLayers], beta[kSmallLayers], ldj_const[kSmallLayers];
     float xmin[kSmallLayers][8], xmax[kSmallLayers][8];  // NormalizationLayer bounds (d <= 8)
-    float tmin[8], tmax[8];                              // θ bounds (n <= 8)
-    int32_t norm_theta;                                  // θ raw: normalise it with tmin / tmax
+    // (the θ bounds are NOT here: the kernel reads them through ChainArgs::tmin / tmax, the
+    // chain's device copy, so a captured train step sees df_chain_set_theta_bounds)
 };
 // nw = 2 (default): the s- and t-nets of a layer on two waves of the workgroup; 1: one wave
 hipError_t launch_small(int mode, const ChainArgs& a, const SmallDesc& sd, unsigned grid, hipStream_t st,

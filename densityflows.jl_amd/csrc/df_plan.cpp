@@ -1073,8 +1073,9 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err, int exact
             P.tiles -= P.tiles % P.tile_group;
         }
         P.samples_per_block = kWavesPerBlock * 16 * P.tiles;
-        if ((int)(P.tables.size() + P.params.size()) > kMaxTableInts)
-            fail(DF_ERR_UNSUPPORTED, "chain index tables and NormalizationLayer bounds exceed 16 KiB");
+        if (table_lds_ints(P) > kMaxTableInts)
+            fail(DF_ERR_UNSUPPORTED, params_in_lds(P) ? "chain index tables and NormalizationLayer bounds exceed 16 KiB"
+                                                      : "chain index tables exceed 16 KiB");
         if (P.stages.empty()) {  // normalization-only chain: keep one empty stage record
             P.stage_max = 0;
         }

@@ -259,8 +259,13 @@ int build_plan(const df_chain_desc* desc, Plan* out, std::string* err, int exact
 
 // Workgroup LDS bytes for a plan (stage buffers + tables + state tile).
 size_t plan_lds_bytes(const Plan& p);
-// LDS bytes of the table area: the index tables, then the NormalizationLayer bounds
-// (`params`), which the specialised kernel copies next to them (ChainArgs::n_par).
-inline int table_lds_bytes(const Plan& p) { return (int)(((p.tables.size() + p.params.size()) * 4 + 15) / 16 * 16); }
+// The NormalizationLayer bounds (`params`) are copied into LDS next to the index tables
+// only by the specialised kernel's one-pass copy-in (df_uniform_impl.h fast_copy, which
+// needs n_par <= kBlockThreads); every other plan keeps them in HBM.
+inline bool params_in_lds(const Plan& p) { return p.uniform && p.params.size() <= (size_t)kBlockThreads; }
+// int32 words of the table area: the index tables, then (params_in_lds) the bounds
+inline int table_lds_ints(const Plan& p) { return (int)(p.tables.size() + (params_in_lds(p) ? p.params.size() : 0)); }
+// LDS bytes of the table area
+inline int table_lds_bytes(const Plan& p) { return (table_lds_ints(p) * 4 + 15) / 16 * 16; }
 
 }  // namespace df

@@ -1,20 +1,27 @@
 // df_small.hip — the small-batch chain kernel.
 //
 // For a batch that leaves most of the chip idle (config 1 at its stated B = 4096:
-// 128 tiles of 32 samples for 1024 SIMDs) a launch lasts as long as ONE wave's
-// dependent chain through the layers.  The specialised kernel's chain is long
-// (profiles/r04_phase_cfg1.txt, in-kernel phase stamps of workgroup 0): three
-// serial global round trips to copy the tables and the state tile in, two LDS
-// round trips per feature read, coupling update and ldj update of every net, a
-// barrier per stage switch and before the copy-out.  This kernel removes all of
-// it: one wave per workgroup, two 16-sample tiles per wave, and
-//   * every lane holds the whole state row of its sample, vcat(θ, z) plus the
-//     zero slot and the 1 of the folded first-Dense bias, in registers; the
-//     conditioner features are register selects, the coupling updates the row
-//     in place (RNVP.jl:182-184 / 86-90), the ldj accumulators are registers;
-//   * the weight fragments of the next layer's nets are loaded from the blob (the
-//     same bytes the LDS stages hold) into registers while the current layer runs;
-//   * no LDS, no barrier; the outputs are stored from registers.
+// 256 workgroups of 16 samples for 256 CUs) a launch lasts as long as one
+// workgroup's dependent chain through the layers.  The specialised kernel's chain is
+// long: serial global round trips to copy the tables and the state tile in, LDS round
+// trips per feature read, a barrier per stage switch and before the copy-out.  This
+// kernel shortens it:
+//   * one 16-sample tile per workgroup, on two waves (NW = 2, the default): the
+//     s-net of every layer runs on wave 0 and the t-net on wave 1 (the two nets of a
+//     layer read the same features, RNVP.jl:174-177, and are independent); wave 1
+//     hands its outputs to wave 0 in LDS, wave 0 applies the coupling (RNVP.jl:182-184
+//     / 86-90) and keeps the ldj in registers, and a bare barrier (lgkmcnt(0) +
+//     s_barrier) after each layer gives wave 1 the updated row.  NW = 1
+//     (DF_SMALL_WAVES=1) runs both nets on one wave, no barrier;
+//   * the state rows of the tile, vcat(θ, z) plus the zero slot and the 1 of the
+//     folded first-Dense bias, sit in a 16 × 13-float LDS patch;
+//   * every layer's net fragments are loaded from the blob (the same bytes the LDS
+//     stages of the specialised kernel hold) into registers at kernel start, with the
+//     rows and the θ bounds, so all loads are in flight before the first use;
+//   * the per-layer fields (blob offsets, feature / transformed-dim slots, kinds,
+//     element flags, NormalizationLayer bounds) come in a SmallDesc passed by value
+//     and held in two VGPRs (v_readlane per field); the θ bounds are read through
+//     ChainArgs::tmin / tmax, the chain's device copy.
 // The arithmetic is the FAST variant's, operation for operation: the first Dense
 // as one f32 MFMA k-step with the bias folded in, the hidden Dense as the
 // k-ordered f32 MFMA chain, bias then relu, the output Dense as the VALU GEMV
@@ -22,7 +29,8 @@
 // rounded as z·exp(s), + t (forward) and (x − t), ·exp(−s) (inverse), Σ s in row
 // order, the ldj grouped per FlowElement (Blocks.jl:136,149, Chains.jl:160,179) —
 // so its outputs are bitwise those of the FAST kernel.  The one difference is the
-// order of the fp64 NLL partial sums (per workgroup of 32 samples).
+// order of the fp64 NLL partial sums (one partial per workgroup of 16 samples).
+// Phase stamps of the one-wave form: profiles/r04_phase_small_v2.txt.
 #include "df_uniform_impl.h"
 
 namespace df {
@@ -72,7 +80,7 @@ struct DescRegs {
     __device__ __forceinline__ float f32(int byte) const { return __uint_as_float(u32(byte)); }
 };
 #define SD_OFF(f) ((int)offsetof(SmallDesc, f))
-static_assert(offsetof(SmallDesc, norm_theta) <= 128 * 4, "DescRegs holds the first 128 dwords");
+static_assert(sizeof(SmallDesc) <= 128 * 4, "DescRegs holds the whole descriptor (128 dwords)");
 
 // net k (0 = s, 1 = t) of layer li: its fragments at the blob offsets of the descriptor
 __device__ __forceinline__ void load_net(const ChainArgs& a, const SmallDesc& sd, int li, int k, NetW& w) {
@@ -156,10 +164,12 @@ __global__ void __launch_bounds__(64 * NW, 1) small_kernel(ChainArgs a, SmallDes
     float* row = srow + j * kStride;
 
     // every load in flight before the first use: the row (lane group g: columns g, g + 4,
-    // g + 8), then every coupling net's fragments
-    // branch-free: a clamped address always, the value selected afterwards
-    float rv[3];
+    // g + 8) with the θ bounds of its θ columns (ChainArgs::tmin / tmax, the chain's device
+    // copy: a captured train step reads the current bounds), then every coupling net's
+    // fragments; branch-free: a clamped address always, the value selected afterwards
+    float rv[3], blo[3], bhi[3];
     const int64_t sv = valid ? smp : 0;
+    const bool norm_th = a.tmin != nullptr;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
         const int c = g + 4 * q;
@@ -167,6 +177,11 @@ __global__ void __launch_bounds__(64 * NW, 1) small_kernel(ChainArgs a, SmallDes
         const float* p = is_th ? a.theta + sv * n + c : a.zin + sv * d + (is_z ? c - n : 0);
         const float v = *p;
         rv[q] = ((is_th || is_z) && valid) ? v : (c == nd + 3 ? 1.f : 0.f);
+        if (norm_th) {
+            const int cb = is_th ? c : 0;
+            blo[q] = a.tmin[cb];
+            bhi[q] = a.tmax[cb];
+        }
     }
     DescRegs dr;
     {
@@ -187,14 +202,9 @@ __global__ void __launch_bounds__(64 * NW, 1) small_kernel(ChainArgs a, SmallDes
     for (int q = 0; q < 3; ++q) {
         const int c = g + 4 * q;
         float v = rv[q];
-        if (c < n && sd.norm_theta && valid) {  // normalize_input (Data.jl:213-218)
-            const int q4 = 4 * (q == 0 ? 0 : 1);
-            const float lo = by_group(g, dr.f32(SD_OFF(tmin) + 4 * q4), dr.f32(SD_OFF(tmin) + 4 * (q4 + 1)),
-                                      dr.f32(SD_OFF(tmin) + 4 * (q4 + 2)), dr.f32(SD_OFF(tmin) + 4 * (q4 + 3)));
-            const float hi = by_group(g, dr.f32(SD_OFF(tmax) + 4 * q4), dr.f32(SD_OFF(tmax) + 4 * (q4 + 1)),
-                                      dr.f32(SD_OFF(tmax) + 4 * (q4 + 2)), dr.f32(SD_OFF(tmax) + 4 * (q4 + 3)));
-            const float diff = hi - lo;
-            v = (diff == 0.f) ? 0.f : (v - lo) / diff;
+        if (c < n && norm_th && valid) {  // normalize_input (Data.jl:213-218)
+            const float diff = bhi[q] - blo[q];
+            v = (diff == 0.f) ? 0.f : (v - blo[q]) / diff;
         }
         if (c < kStride) row[c] = v;
     }

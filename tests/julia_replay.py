@@ -25,6 +25,7 @@ import numpy as np
 
 from densityflows_amd import _lib
 from densityflows_amd.hip import _Desc, chain_dims, flatten_elements
+from densityflows_amd.train import _dense_order
 from densityflows_amd.train import trainables as _flux_trainables
 
 CALLS: list = []
@@ -392,6 +393,33 @@ def train_step_graph_bang(t, x_ptr, th_ptr, B, stream=NULL):
     check(cc("df_train_step_graph", t.handle, x_ptr, th_ptr, C.c_int64(B), C.c_int64(B), NULL, stream),
           "df_train_step_graph")
     return None
+
+
+# ---- weight export (copy_trainables!) ------------------------------------------------------
+def _flux_trainables_arrays(model):
+    """Flux.trainables(model) of the Python mirror: the arrays in the order Functors walks
+    them (FlowChain elements; per coupling layer s_net then t_net, trainable=(s_net,
+    t_net) in src/affine/RNVP.jl:51, NICE t_net only, NormalizationLayer none; per Dense
+    weight then bias), each as (Dense, field name)."""
+    for D in _dense_order(model.layers):
+        yield D, "W"
+        if D.b is not None:
+            yield D, "b"
+
+
+def copy_trainables_bang(model, p):
+    """copy_trainables!(model, p): `copyto!(a, 1, p, off + 1, n)` into each trainable array
+    (a Julia array fills column-major), then the length check."""
+    p = np.asarray(p, np.float32)
+    off = 0
+    for D, name in _flux_trainables_arrays(model):
+        a = getattr(D, name)
+        n = a.size
+        setattr(D, name, p[off:off + n].reshape(a.shape, order="F").copy())
+        off += n
+    if off != len(p):
+        raise _lib.DimensionMismatch(f"model has {off} trainables, device vector {len(p)}")
+    return model
 
 
 # ---- multi-GPU (comm_unique_id, HIPComm, flow_nll, train_step_dist!) ---------------------

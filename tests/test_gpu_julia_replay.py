@@ -125,6 +125,32 @@ def test_julia_sample_train_sample_sequence(cuda):
         assert ok, ("sample after train!", r)
         assert not np.array_equal(s0, s1)
 
+        # 3b. weight export (src/Loading.jl:78-96,324-346): the device vector
+        # written into a FRESH mirror model by copy_trainables! (Flux.trainables order), a
+        # chain re-created from that model, and its forward bitwise the trained chain's
+        _, chain_new, _ = _datatest_flow(seed=99)            # same structure, other weights
+        assert not np.array_equal(trainables(chain_new), c.params)
+        J.copy_trainables_bang(chain_new, c.params)
+        np.testing.assert_array_equal(trainables(chain_new), c.params)
+        for D_new, D_py in zip(chain_new.layers[0].s_net, chain2.layers[0].s_net):  # per Dense, mirror walk
+            np.testing.assert_array_equal(D_new.W, D_py.W)
+        c_new = J.HIPFlowChain(chain_new)
+        try:
+            x_tr, th_tr = data.training_data()
+            thn_tr = J.normalize_input(th_tr, md.theta_min, md.theta_max)
+            xa, la = J.forward(c, x_tr, thn_tr)
+            xb_, lb_ = J.forward(c_new, x_tr, thn_tr)
+            np.testing.assert_array_equal(xa, xb_)
+            np.testing.assert_array_equal(la, lb_)
+            za, lza = J.backward(c, x_tr, thn_tr)
+            zb2, lzb = J.backward(c_new, x_tr, thn_tr)
+            np.testing.assert_array_equal(za, zb2)
+            np.testing.assert_array_equal(lza, lzb)
+        finally:
+            c_new.finalize()
+        with pytest.raises(AssertionError):                  # DimensionMismatch on a short vector
+            J.copy_trainables_bang(chain_new, c.params[:-1])
+
         # 4. the model-level calls the shim exposes, θ as given, bounds still set
         x_va, th_va = data.validation_data()
         thn_va = J.normalize_input(th_va, md.theta_min, md.theta_max)
@@ -196,6 +222,17 @@ def test_trainer_theta_input_modes(cuda):
     a.chain.set_theta_bounds(tmin, tmax)
     b.chain.set_theta_bounds(tmin, tmax)
     tb.copy_(tb_raw)                                      # same buffer, raw θ now
+    for _ in range(3):
+        a.step_graph(xb, tb, 512)
+        b.step(xb, tb, 512)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(a.get_params(), b.get_params())
+    # new bounds under the same convention (AUTO, bounds set before
+    # and after) keep the capture; its replays must read the NEW bounds in every kernel
+    # (the small-batch inverse pass included: batch 512 of the README chain runs on it)
+    tmin2, tmax2 = np.array([-3.0], np.float32), np.array([0.5], np.float32)
+    a.chain.set_theta_bounds(tmin2, tmax2)
+    b.chain.set_theta_bounds(tmin2, tmax2)
     for _ in range(3):
         a.step_graph(xb, tb, 512)
         b.step(xb, tb, 512)

@@ -184,3 +184,35 @@ def test_model_level_calls_take_theta_as_given(shim):
     assert re.search(r"const DF_THETA_GIVEN = Cint\(2\)", shim)
     flow_syms = {s for v in jl.values() for s in v if s.startswith("df_flow_")}
     assert flow_syms == {"df_flow_sample"}, flow_syms
+
+
+def test_weight_export_walks_flux_trainables(shim):
+    """copy_trainables! and hip_flow call no C entry point, so the ccall replay check
+    above does not see them.  The order contract, statically:
+      * HIPFlowChain hands the device the model's parameters as
+        vcat(vec.(Flux.trainables(chain))) and copy_trainables! writes them back with the
+        same walk over Flux.trainables(model), column-major copyto! per array, checking
+        the total length;
+      * tests/julia_replay.py has a replay of copy_trainables! (run on the GPU by
+        test_gpu_julia_replay.py: trained vector → fresh model → re-created chain,
+        bitwise the trained chain's forward / backward);
+      * hip_flow goes through the reference's own reader (DensityFlows.load_flow,
+        src/Loading.jl:348-377) and wraps f.model as FlowChain((HIPFlowChain(f.model),)).
+    """
+    import ast
+
+    body = re.search(r"function copy_trainables!\(model::FlowChain, p::Vector\{Float32\}\)(.*?)\nend", shim, re.S)
+    assert body, "copy_trainables! not found"
+    b = body.group(1)
+    assert re.search(r"for a in Flux\.trainables\(model\)", b)
+    assert "copyto!(a, 1, p, off + 1, n)" in b and "off += n" in b
+    assert re.search(r"off == length\(p\) \|\| throw\(DimensionMismatch", b)
+    hc = re.search(r"function HIPFlowChain\(chain::FlowChain;.*?\nend", shim, re.S)
+    assert hc and re.search(r"reduce\(vcat, \[vec\(Float32\.\(a\)\) for a in Flux\.trainables\(chain\)\]\)", hc.group(0))
+    hf = re.search(r"function hip_flow\(directory::AbstractString;.*?\nend", shim, re.S)
+    assert hf and "DensityFlows.load_flow(directory)" in hf.group(0)
+    assert "FlowChain((HIPFlowChain(f.model; device = device),))" in hf.group(0)
+    with open(os.path.join(ROOT, "tests", "julia_replay.py")) as f:
+        tree = ast.parse(f.read())
+    names = {n.name for n in tree.body if isinstance(n, ast.FunctionDef)}
+    assert "copy_trainables_bang" in names
