@@ -440,7 +440,8 @@ namespace df {
 namespace api {
 
 int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, float* xout, float* ldj, float* lp,
-        double* sum_out, int64_t batch, void* stream, float* snap, float* hsave, int hsave_w, int hsave_h) {
+        double* sum_out, int64_t batch, void* stream, float* snap, float* hsave, int hsave_w, int hsave_h,
+        float* fsave) {
     if (!c) return set_err(DF_ERR_INVALID, "null chain");
     if (batch < 0) return set_err(DF_ERR_SHAPE, "negative batch size");
     const df::Plan& P = c->plan;
@@ -463,6 +464,8 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     const bool wide = P.wide && !c->no_wide;
     const bool split = !wide && use_split(c);
     const bool small = !wide && !split && use_small(c, batch);
+    if (fsave && !(wide && use_wsplit(c)))  // the trainer plans its H0-free sweep on the wide SPLIT kernel
+        return set_err(DF_ERR_INVALID, "internal: feature snapshots need the wide SPLIT kernel");
     // (the small kernel runs one 16-sample tile per workgroup: tiles = 1, only reported)
     const int tiles = wide ? df::kWideT : small ? 1 : choose_tiles(c, mode, batch, split);
     {
@@ -545,6 +548,7 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
     a.hsave = P.uniform ? nullptr : hsave;
     a.hsave_w = hsave_w;
     a.hsave_h = hsave_h;
+    a.fsave = nullptr;
 
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipError_t e;
@@ -568,6 +572,7 @@ int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, 
             a.tables = static_cast<const int32_t*>(c->d_wstables);
             a.tab_ints = (int)P.wstables.size();
             a.tab_bytes = c->wstab_bytes;
+            a.fsave = fsave;  // features instead of H0 (the split kernel only)
             e = df::launch_wide(mode, a, (unsigned)grid, c->wslds, st, true);
         } else {
             e = df::launch_wide(mode, a, (unsigned)grid, c->wide_lds, st);

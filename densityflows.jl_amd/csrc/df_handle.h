@@ -129,7 +129,7 @@ double* train_last_lpsum(df_train* t);
 // snap (inverse modes, specialised kernel): every layer's output kept.
 int run(df_chain* c, int mode, bool flow, const float* zin, const float* theta, float* xout, float* ldj, float* lp,
         double* sum_out, int64_t batch, void* stream, float* snap = nullptr, float* hsave = nullptr,
-        int hsave_w = 0, int hsave_h = 0);
+        int hsave_w = 0, int hsave_h = 0, float* fsave = nullptr);
 
 }  // namespace api
 }  // namespace df

@@ -48,6 +48,9 @@ struct ChainArgs {
     float* hsave;        // inverse modes, generic kernel: hidden activations of every net,
                          // [(layer·2 + net)·hsave_h + k][sample][hsave_w] (training, layer-wise path)
     int hsave_w, hsave_h;
+    float* fsave;        // inverse modes, wide SPLIT kernel (training, H0 recomputed): the first
+                         // Dense's input vcat(θ, u)[axis_nn] of every net, [layer·2 + net][sample][32],
+                         // and hsave then keeps H1 only (hsave_h = 1)
     const WLayer* wlayers;   // wide-net kernel only (stages / blob / schedules then refer to the wide blob)
     const float* wbias;
     uint64_t* clk;           // effective-clock stamps (df_chain_clock_probe), nullptr = off

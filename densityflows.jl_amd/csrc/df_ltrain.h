@@ -88,6 +88,8 @@ struct LDenseArgs {
     const uint8_t* w0t;
     int w0t_mt, w0t_nkq;
     const uint8_t* w0s;     // SPLIT instances: W0ᵀ as bf16x3 planes [c][m][p][lane][8] (x̄ on bf16 MFMA), or nullptr
+    const uint32_t* hmask;  // LEPI_DACT(_XBAR), relu: σ'(H) from a relu mask [B][8] words (16 bits per m-tile:
+                            // bit j of m-tile m ↔ row 16m + j; written by the H0-recomputing split dW1), else hprev
     // couple_bwd_kernel: second product W_outᵀ ȳ (fragments [kq][m][lane][4], m < 16·HT rows)
     const uint8_t* w2frag;
     int nkq2;
@@ -106,6 +108,14 @@ struct LdwArgs {
     int w_off, b_off;       // trainables offsets (b_off -1: no bias)
     int64_t batch;
     int split;              // 1: bf16x3 split products (ldw_split_kernel, its own launch; mta = ntb = 16)
+    // split dW1 with H0 recomputed (xb unused): H0 = relu(b0 + W0·f) with the wide SPLIT
+    // kernel's first-Dense arithmetic (bitwise its H0), f the net's features [B][32]
+    // (ChainArgs::fsave), W0 the first-Dense stage [m < 16][p][lane][8] of the wide split
+    // blob; the kernel also writes H0's relu mask for the W1ᵀδ1 epilogue
+    const float* feat;
+    const uint8_t* w0s;
+    const float* b0;
+    uint32_t* hmask;        // [B][8]: 16 bits per m-tile m, bit j ↔ H0 row 16m + j > 0
 };
 
 // One merged launch: up to three non-split dW products (ldw) of net i and, optionally, the

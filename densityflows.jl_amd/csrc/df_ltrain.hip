@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
                     load_x(2 * c + 3, xn1);
                 }
                 if constexpr (kDact) {
-                    if (c + 1 == nchunks) {
+                    if (c + 1 == nchunks && !a.hmask) {
 #pragma unroll
                         for (int m = 0; m < HR; ++m)
                             h0[m] = *reinterpret_cast<const f32x4*>(a.hprev + s0h * a.ld_h + 4 * g + 16 * m);
@@ -230,6 +230,25 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
                 // the σ' arguments of the whole tile are loaded at once (a padding
                 // sample reads the last row; its δ is zeroed and never stored)
                 const int64_t s = valid[t] ? smp[t] : a.batch - 1;
+                if (a.hmask) {  // relu σ' from the mask of the H0-recomputing split dW1 (no H read)
+                    uint32_t mk[8];
+                    {
+                        const uint4* mp = reinterpret_cast<const uint4*>(a.hmask + s * 8);
+                        const uint4 u0 = mp[0], u1 = mp[1];
+                        mk[0] = u0.x; mk[1] = u0.y; mk[2] = u0.z; mk[3] = u0.w;
+                        mk[4] = u1.x; mk[5] = u1.y; mk[6] = u1.z; mk[7] = u1.w;
+                    }
+#pragma unroll
+                    for (int m = 0; m < MT; ++m) {
+                        f32x4 v = acc[t][m];
+                        const uint32_t bits = mk[m >> 1] >> (16 * (m & 1) + 4 * g);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) v[q] = ((bits >> q) & 1u) ? v[q] : 0.f;
+                        if (!valid[t]) v = f32x4{0.f, 0.f, 0.f, 0.f};
+                        else *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + 16 * m + 4 * g) = v;
+                        if constexpr (EPI == LEPI_DACT_XBAR) acc[t][m] = v;  // δ0 → B operand of W0ᵀ
+                    }
+                } else {
                 const float* hrow = a.hprev + s * a.ld_h + 4 * g;
                 f32x4 h[HR];
 #pragma unroll
@@ -249,6 +268,7 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
                     if (!valid[t]) v = f32x4{0.f, 0.f, 0.f, 0.f};
                     else *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + 16 * m + 4 * g) = v;
                     if constexpr (EPI == LEPI_DACT_XBAR) acc[t][m] = v;  // δ0 → B operand of W0ᵀ
+                }
                 }
                 if constexpr (EPI == LEPI_DACT_XBAR) {
                     // x̄ = W0ᵀ δ0 (rows = conditioner features, <= 4 tiles) → z̄ of identity dims
@@ -678,9 +698,23 @@ __device__ __forceinline__ void ldw_body(const LdwArgs& a, float* lsm, int bid, 
 #ifndef DF_LDW_DIAG
 #define DF_LDW_DIAG 0
 #endif
+#ifndef DF_LDW_H0_HALVES
+#define DF_LDW_H0_HALVES 0
+#endif
 #if DF_LDW_DMA
 __device__ __forceinline__ int ldw_slot(int row, int sg) { return sg ^ ((-(row >> 2)) & 3); }
 
+// H0R (training with feature snapshots, LdwArgs::feat): the second operand, H0, is not
+// read from HBM but recomputed per step from the net's 32-float feature rows with the wide
+// SPLIT kernel's first-Dense products (bias, then w2·x0, w1·x1, w0·x2, w1·x0, w0·x1, w0·x0
+// onto one accumulator, relu).  The product runs transposed — features as the A operand,
+// the W0 fragments (the same bytes) as B — so a lane ends with one H0 row for four
+// consecutive samples and writes its bf16x3 planes straight into the B planes (8 bytes
+// a plane; no f32 stage, no second split pass).  Wave w computes m-tiles 4w .. 4w + 3 of
+// both 16-sample tiles (its 12 W0 fragments and 4 bias values stay in registers), during
+// the split phase of the step; the step's feature loads are issued one step ahead.  It
+// also writes H0's relu mask for the W1ᵀδ1 epilogue (one ballot per row quad).
+template <bool H0R>
 __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lsm_f[];
     constexpr int PB = 256 * 64;  // bytes per plane
@@ -703,11 +737,12 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
         for (int in = 0; in < 8; ++in) acc[im][in] = f32x4{0.f, 0.f, 0.f, 0.f};
     float dbp[4] = {0.f, 0.f, 0.f, 0.f};  // rows q + 64i, sample group sg
 
-    // sample rows s = wave, wave + 4, .. of both operands (64 per step); a sample past
-    // the workgroup's range is a row of zeros instead
+    constexpr int NM = H0R ? 4 : 1;  // H0R: m-tiles 4·wave + mm of H0 per wave
+    // sample rows s = wave, wave + 4, .. of both operands (64 per step; H0R: δ only, 32); a
+    // sample past the workgroup's range is a row of zeros instead
     auto dma = [&](int64_t s0) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
+        for (int k = 0; k < (H0R ? 8 : 16); ++k) {
             const int r = wave + 4 * k, op = r >> 5, s = r & 31;
             float* dst = stage + (op * 32 + s) * 256;
             if (s0 + s < s_end) {
@@ -719,17 +754,111 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
             }
         }
     };
+    // H0R: this wave's W0 fragments (B operand: lane (g, j) holds W0[16mt + j][8g + e]) and
+    // bias values b0[16mt + j], m-tiles mt = 4·wave + mm.  Re-read each step at its top (L2
+    // hits: 48 KiB read by every workgroup), their latency under the δ split: held through
+    // the MFMA phase they would spill.  The pointers are opaque per step (as loop invariants
+    // the loads would be hoisted out of the loop).
+    struct W0In {
+        uni::bf16x8 w[NM][3];
+        float b[NM];
+    };
+    auto h0_wload = [&](W0In& in) {
+        const uint8_t* w0p = a.w0s;
+        const float* b0p = a.b0;
+        asm volatile("" : "+s"(w0p), "+s"(b0p));
+#pragma unroll
+        for (int mm = 0; mm < NM; ++mm) {
+            const int mt = 4 * wave + mm;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                in.w[mm][p] = *reinterpret_cast<const uni::bf16x8*>(w0p + ((mt * 3 + p) << 10) + lane * 16);
+            in.b[mm] = b0p[16 * mt + j];
+        }
+    };
+    // H0R: features of samples s0 + 16tt + j (lane group g: 8g .. 8g + 7; past the range:
+    // any row, the H0 values are zeroed)
+    auto h0_load = [&](int64_t s0, f32x4 (&fr)[2][2]) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            const int64_t s = s0 + 16 * tt + j;
+            const int64_t sc = s < s_end ? s : s_begin;
+            const f32x4* fp = reinterpret_cast<const f32x4*>(a.feat + sc * 32 + 8 * g);
+            fr[tt][0] = fp[0];
+            fr[tt][1] = fp[1];
+        }
+    };
+    auto h0_compute = [&](int64_t s0, const f32x4 (&fr)[2][2], const W0In& w0) {
+        uni::bf16x8 x[2][3];  // A operand: lane (g, i) holds features 8g + e of sample 16tt + i
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            const float v[8] = {fr[tt][0][0], fr[tt][0][1], fr[tt][0][2], fr[tt][0][3],
+                                fr[tt][1][0], fr[tt][1][1], fr[tt][1][2], fr[tt][1][3]};
+            uni::split8(v, x[tt][0], x[tt][1], x[tt][2]);
+        }
+        // mask word of this lane: sample sl = lane & 31 of the step, m-tiles 4w + 2mp, + 1
+        const int sl = lane & 31, mp = lane >> 5;
+        uint32_t mword = 0u;
+#pragma unroll
+        for (int mp2 = 0; mp2 < 2; ++mp2) {
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt) {
+                float hv[8];  // rows 16(4w + 2mp2 + hh) + j, samples 16tt + 4g + r: hv[4hh + r]
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int mm = 2 * mp2 + hh;
+                    f32x4 v = f32x4{w0.b[mm], w0.b[mm], w0.b[mm], w0.b[mm]};
+                    v = uni::mfma_bf(x[tt][0], w0.w[mm][2], v);
+                    v = uni::mfma_bf(x[tt][1], w0.w[mm][1], v);
+                    v = uni::mfma_bf(x[tt][2], w0.w[mm][0], v);
+                    v = uni::mfma_bf(x[tt][0], w0.w[mm][1], v);
+                    v = uni::mfma_bf(x[tt][1], w0.w[mm][0], v);
+                    v = uni::mfma_bf(x[tt][0], w0.w[mm][0], v);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const bool ok = s0 + 16 * tt + 4 * g + r < s_end;
+                        const float h = ok ? uni::relu_fast(v[r]) : 0.f;
+                        hv[4 * hh + r] = h;
+                        // lane group g' of the ballot: rows 16mt + 0..15 of sample 16tt + 4g' + r
+                        const uint64_t bal = __ballot(h > 0.f);
+                        if ((sl >> 4) == tt && (sl & 3) == r && mp == mp2)
+                            mword |= (uint32_t)((bal >> (16 * ((sl >> 2) & 3))) & 0xffffu) << (16 * hh);
+                    }
+                }
+                uni::bf16x8 p[3];
+                uni::split8(hv, p[0], p[1], p[2]);
+                const int sgp = 2 * tt + (g >> 1);  // 8-sample group of samples 16tt + 4g ..
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int row = 16 * (4 * wave + 2 * mp2 + hh) + j;
+                    uint8_t* dst = TB + row * 64 + 16 * ldw_slot(row, sgp) + 8 * (g & 1);
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        uint64_t u[2];
+                        __builtin_memcpy(u, &p[k], 16);
+                        *reinterpret_cast<uint64_t*>(dst + k * PB) = u[hh];
+                    }
+                }
+            }
+        }
+        const int64_t s = s0 + sl;
+        if (s < s_end) reinterpret_cast<uint32_t*>(a.hmask)[s * 8 + 2 * wave + mp] = mword;
+    };
     // step 2 for one operand: rows 4q + i, samples 8sg + e
     // Rows q + 64i (not 4q + i): the 16 lanes of a plane write then cover all 16
     // (row & 3, slot) pairs, i.e. all 64 banks (rows 4 apart sit 256 B apart: one bank
     // group per slot, 16-way).  The stage reads become dword reads of 64 consecutive
-    // floats (conflict-free).
-    auto split_item = [&](int op, uint8_t* T, bool db) {
+    // floats (conflict-free).  swz: the H0R rows (quad XOR (s & 15)).
+    auto split_item = [&](int op, uint8_t* T, bool db, bool swz) {
         float x[4][8];
 #pragma unroll
         for (int e = 0; e < 8; ++e)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) x[i][e] = stage[(op * 32 + 8 * sg + e) * 256 + q + 64 * i];
+            for (int i = 0; i < 4; ++i) {
+                const int s = 8 * sg + e;
+                const int r = swz ? ((q + 64 * i) ^ ((s & 15) << 2)) : q + 64 * i;
+                x[i][e] = stage[(op * 32 + s) * 256 + r];
+            }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const float(&v)[8] = x[i];
@@ -754,35 +883,57 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
         for (int k = 0; k < 3; ++k) p[k] = *reinterpret_cast<const uni::bf16x8*>(src + k * PB);
     };
 
-    if (s_begin < s_end) dma(s_begin);
+    [[maybe_unused]] f32x4 fr[2][2];
+    if (s_begin < s_end) {
+        if constexpr (H0R) h0_load(s_begin, fr);
+        dma(s_begin);
+    }
     for (int64_t s0 = s_begin; s0 < s_end; s0 += 32) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's rows of the step landed
         __syncthreads();                                     // ... every wave's; the planes are free
 #if DF_LDW_DIAG != 2
-        split_item(0, TA, true);
-        split_item(1, TB, false);
+        if constexpr (H0R) {
+            W0In w0;
+            h0_wload(w0);  // in flight through the δ split
+            split_item(0, TA, true, false);
+            h0_compute(s0, fr, w0);
+        } else {
+            split_item(0, TA, true, false);
+            split_item(1, TB, false, false);
+        }
 #endif
         __syncthreads();                                     // planes written; the stage is free
-        if (s0 + 32 < s_end) dma(s0 + 32);
+        const bool more = s0 + 32 < s_end;
+        if constexpr (H0R) {
+            if (more) h0_load(s0 + 32, fr);  // in flight through the MFMA phase
+        }
+        if (more) dma(s0 + 32);
 #if DF_LDW_DIAG == 1
         continue;
 #endif
-        uni::bf16x8 xb[8][3];
+        // (DF_LDW_H0_HALVES=1, H0R: the column fragments in two halves of 4 — fewer registers
+        // through the phase, twice the row-fragment reads; the same products in the same
+        // order per accumulator)
+        constexpr int NH = (H0R && DF_LDW_H0_HALVES) ? 2 : 1, NI = 8 / NH;
 #pragma unroll
-        for (int in = 0; in < 8; ++in) frag(TB, 16 * (n0 + in) + j, xb[in]);
+        for (int hv = 0; hv < NH; ++hv) {
+            uni::bf16x8 xb[NI][3];
 #pragma unroll
-        for (int im = 0; im < 8; ++im) {
-            uni::bf16x8 wa[3];
-            frag(TA, 16 * (m0 + im) + j, wa);
+            for (int in = 0; in < NI; ++in) frag(TB, 16 * (n0 + NI * hv + in) + j, xb[in]);
 #pragma unroll
-            for (int in = 0; in < 8; ++in) {  // small terms first
-                f32x4 v4 = acc[im][in];
-                v4 = uni::mfma_bf(wa[2], xb[in][0], v4);
-                v4 = uni::mfma_bf(wa[1], xb[in][1], v4);
-                v4 = uni::mfma_bf(wa[0], xb[in][2], v4);
-                v4 = uni::mfma_bf(wa[1], xb[in][0], v4);
-                v4 = uni::mfma_bf(wa[0], xb[in][1], v4);
-                acc[im][in] = uni::mfma_bf(wa[0], xb[in][0], v4);
+            for (int im = 0; im < 8; ++im) {
+                uni::bf16x8 wa[3];
+                frag(TA, 16 * (m0 + im) + j, wa);
+#pragma unroll
+                for (int in = 0; in < NI; ++in) {  // small terms first
+                    f32x4 v4 = acc[im][NI * hv + in];
+                    v4 = uni::mfma_bf(wa[2], xb[in][0], v4);
+                    v4 = uni::mfma_bf(wa[1], xb[in][1], v4);
+                    v4 = uni::mfma_bf(wa[0], xb[in][2], v4);
+                    v4 = uni::mfma_bf(wa[1], xb[in][0], v4);
+                    v4 = uni::mfma_bf(wa[0], xb[in][1], v4);
+                    acc[im][NI * hv + in] = uni::mfma_bf(wa[0], xb[in][0], v4);
+                }
             }
         }
     }
@@ -929,6 +1080,15 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
 
 #endif  // DF_LDW_DMA
 
+void* ldw_split_ptr(bool h0r) {
+#if DF_LDW_DMA
+    return h0r ? reinterpret_cast<void*>(&ldw_split_kernel<true>) : reinterpret_cast<void*>(&ldw_split_kernel<false>);
+#else
+    (void)h0r;
+    return reinterpret_cast<void*>(&ldw_split_kernel);
+#endif
+}
+
 template <int S, int BMX, int BNX>
 __global__ void __launch_bounds__(kBlockThreads, 1) ldw_kernel(LdwArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lsm[];
@@ -1054,9 +1214,12 @@ hipError_t set_ldense_lds_limit(size_t lds) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_kernel<32, kLdwBM, kLdwBN>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldw_lds_bytes());
     if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_split_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kLdwSplitLds);
+    e = hipFuncSetAttribute(ldw_split_ptr(false), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdwSplitLds);
     if (e != hipSuccess) return e;
+#if DF_LDW_DMA
+    e = hipFuncSetAttribute(ldw_split_ptr(true), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdwSplitLds);
+    if (e != hipSuccess) return e;
+#endif
     return hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_kernel<64, 2, 2>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)ldw_lds_bytes());
 }
@@ -1136,8 +1299,9 @@ hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st) {
     void* args[] = {const_cast<LdwArgs*>(&a)};
     if (a.split) {
         if (a.mta != 16 || a.ntb != 16) return hipErrorInvalidValue;  // the kernel's fixed 256×256 shape
-        return hipLaunchKernel(reinterpret_cast<void*>(&ldw_split_kernel), dim3(grid), dim3(kLdwSplitThreads), args,
-                               kLdwSplitLds, st);
+        const bool h0r = a.feat != nullptr;
+        if (h0r && (!DF_LDW_DMA || !a.w0s || !a.b0 || !a.hmask)) return hipErrorInvalidValue;
+        return hipLaunchKernel(ldw_split_ptr(h0r), dim3(grid), dim3(kLdwSplitThreads), args, kLdwSplitLds, st);
     }
     const int S = ldw_samples(a);
     void* fn = S == 64 ? reinterpret_cast<void*>(&ldw_kernel<64, 2, 2>)

@@ -144,6 +144,13 @@ struct df_train {
     // skips the forward recompute.  [(layer·2 + net)·lmax_h + k][B][lwidth]
     float* d_hsave = nullptr;
     bool hsave_on = false;
+    // H0-free sweep (round 5; wide SPLIT chains of relu hidden-256 nets, DF_TRAIN_H0=1 turns it
+    // off): the inverse pass keeps each net's features vcat(θ, u)[axis_nn] ([layer·2 + net][B][32])
+    // and H1 only (d_hsave with one slot per net); the split dW1 recomputes H0 from the
+    // features and writes its relu mask (d_hmask, [B][8] words) for the W1ᵀδ1 epilogue
+    bool fmode = false;
+    float* d_fsave = nullptr;
+    uint32_t* d_hmask = nullptr;
     // repack maps of the chain's wide-kernel blob and biases (plan.wide)
     void* d_wdst = nullptr;
     void* d_wsrc = nullptr;
@@ -175,7 +182,7 @@ void free_all(df_train* t) {
                     t->d_lblob,  t->d_ldst, t->d_lsrc, t->d_lyp[0], t->d_lyp[1], t->d_lbp[0], t->d_lbp[1], t->d_lx, t->d_hsave,
                     t->d_wdst,   t->d_wsrc, t->d_wbdst, t->d_wbsrc, t->d_sdst, t->d_ssrc,
                     t->d_wsdst, t->d_wssrc, t->d_lsblob, t->d_lsdst, t->d_lssrc,
-                    t->d_tsblob, t->d_tsdst, t->d_tssrc};
+                    t->d_tsblob, t->d_tsdst, t->d_tssrc, t->d_fsave, t->d_hmask};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (float* p : t->d_lh)
@@ -433,6 +440,25 @@ int build_nets(df_train* t) {
     return DF_OK;
 }
 
+// The H0-free sweep (df_train::fmode) applies when the inverse pass runs on the wide SPLIT
+// kernel and every conditioner is its shape: Dense(≤ 32, 256, relu), Dense(256, 256, relu),
+// Dense(256, ≤ 32), with the fused front and the split dW1.
+bool fmode_eligible(const df_train* t) {
+    const df_chain* c = t->c;
+    const Plan& P = c->plan;
+    auto env1 = [](const char* k) { const char* v = std::getenv(k); return v && v[0] == '1'; };
+    if (!t->layerwise || !P.wide || c->no_wide || !use_wsplit(c) || c->exact || P.uniform) return false;
+    if (env1("DF_TRAIN_H0") || env1("DF_TRAIN_NOFUSE") || env1("DF_TRAIN_RECOMPUTE")) return false;
+    for (const LNet& N : t->lnets) {
+        if (N.pre || N.dn.size() != 3) return false;
+        const LDense &D0 = N.dn[0], &D1 = N.dn[1], &D2 = N.dn[2];
+        if (D0.act != DF_ACT_RELU || D1.act != DF_ACT_RELU) return false;
+        if (D0.in_dim > 32 || D0.out_dim != 256 || D1.in_dim != 256 || D1.out_dim != 256) return false;
+        if (D2.fwd.mt > 2 || D0.bwd.mt > 4 || D1.bwd.sfrag < 0) return false;
+    }
+    return true;
+}
+
 int ensure_capacity(df_train* t, int64_t batch) {
     if (batch <= t->cap) return DF_OK;
     t->cap_gen++;  // captured train steps name the old buffers
@@ -444,11 +470,13 @@ int ensure_capacity(df_train* t, int64_t batch) {
         }
     t->cap = 0;
     const int64_t cap = std::max<int64_t>(batch, 1024);
-    for (float** p : {&t->d_lyp[0], &t->d_lyp[1], &t->d_lbp[0], &t->d_lbp[1], &t->d_lx, &t->d_hsave})
+    for (float** p : {&t->d_lyp[0], &t->d_lyp[1], &t->d_lbp[0], &t->d_lbp[1], &t->d_lx, &t->d_hsave, &t->d_fsave})
         if (*p) {
             (void)hipFree(*p);
             *p = nullptr;
         }
+    if (t->d_hmask) (void)hipFree(t->d_hmask);
+    t->d_hmask = nullptr;
     for (auto* v : {&t->d_lh, &t->d_ld, &t->d_lv}) {
         for (float* p : *v)
             if (p) (void)hipFree(p);
@@ -471,11 +499,17 @@ int ensure_capacity(df_train* t, int64_t batch) {
         // kernel and they fit (else the sweep recomputes them)
         t->hsave_on = false;
         if (!P.uniform && !(std::getenv("DF_TRAIN_RECOMPUTE") && std::getenv("DF_TRAIN_RECOMPUTE")[0] == '1')) {
-            const size_t hbytes = row * (size_t)P.n_layers * 2 * t->lmax_h;
+            // fmode: H1 only, plus the 32-float feature rows and the relu-mask buffer
+            const size_t hbytes = row * (size_t)P.n_layers * 2 * (t->fmode ? 1 : t->lmax_h);
+            const size_t fbytes = t->fmode ? sizeof(float) * (size_t)cap * 32 * P.n_layers * 2 : 0;
             size_t free_b = 0, total_b = 0;
-            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && hbytes < free_b / 2 &&
-                hipMalloc(reinterpret_cast<void**>(&t->d_hsave), hbytes) == hipSuccess)
+            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && hbytes + fbytes < free_b / 2 &&
+                hipMalloc(reinterpret_cast<void**>(&t->d_hsave), hbytes) == hipSuccess) {
                 t->hsave_on = true;
+                if (t->fmode && (hipMalloc(reinterpret_cast<void**>(&t->d_fsave), fbytes) != hipSuccess ||
+                                 hipMalloc(reinterpret_cast<void**>(&t->d_hmask), (size_t)cap * 32) != hipSuccess))
+                    return set_err(DF_ERR_NOMEM, "hipMalloc failed (training feature snapshots)");
+            }
             (void)hipGetLastError();
         }
         for (int k = 0; k <= t->lmax_h; ++k) {
@@ -592,6 +626,10 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
     const bool no_fuse = std::getenv("DF_TRAIN_NOFUSE") && std::getenv("DF_TRAIN_NOFUSE")[0] == '1';
     const bool no_merge = std::getenv("DF_TRAIN_NOMERGE") && std::getenv("DF_TRAIN_NOMERGE")[0] == '1';
     auto keeps = [&](const SweepOp& op) { return t->hsave_on && !t->lnets[op.net].pre; };
+    const bool fm = t->fmode && t->hsave_on && t->d_fsave;  // H0-free sweep (struct df_train)
+    auto net_slot = [&](const SweepOp& op) { return 2 * op.layer + (op.phase == TR_PHASE_T ? 1 : 0); };
+    // fmode: the net's feature rows [B][32] (written by the inverse pass)
+    auto fbuf = [&](const SweepOp& op) { return t->d_fsave + (int64_t)net_slot(op) * batch * 32; };
     auto fused_front = [&](const SweepOp& op) {
         const LNet& N = t->lnets[op.net];
         const int nd = (int)N.dn.size();
@@ -599,8 +637,8 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
     };
     // H_k of a net: kept by the inverse pass, or recomputed into the shared buffers
     auto Hbuf = [&](const SweepOp& op, int k) -> float* {
-        const int net_slot = 2 * op.layer + (op.phase == TR_PHASE_T ? 1 : 0);
-        return keeps(op) ? t->d_hsave + ((int64_t)net_slot * t->lmax_h + k) * batch * W : t->d_lh[k];
+        if (fm) return k == 1 ? t->d_hsave + (int64_t)net_slot(op) * batch * W : nullptr;  // H1 only
+        return keeps(op) ? t->d_hsave + ((int64_t)net_slot(op) * t->lmax_h + k) * batch * W : t->d_lh[k];
     };
     // ȳ and the δ of the last hidden Dense alternate between two buffers from net to
     // net: a merged launch writes net i+1's while net i's dW products read net i's
@@ -639,8 +677,8 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             w.lda = W;
             w.m_true = D.out_dim;
             w.mta = D.fwd.mt;
-            w.xb = (k == 0) ? t->d_lx : Hbuf(op, k - 1);
-            w.ldb = W;
+            w.xb = (k == 0) ? (fm ? fbuf(op) : t->d_lx) : Hbuf(op, k - 1);
+            w.ldb = (k == 0 && fm) ? 32 : W;
             w.n_true = D.in_dim;
             w.ntb = D.bwd.mt;
             w.partial = t->d_partial;
@@ -651,6 +689,17 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             if (!ldw_shape(w.mta, w.ntb, &w.wm, &w.bm, &w.bn)) return set_err(DF_ERR_UNSUPPORTED, "dW tiling");
             // hidden-256 × hidden-256 dW on bf16x3 split products (ldw_split_body)
             w.split = (lsplit && w.mta == 16 && w.ntb == 16 && w.bm == kLdwBM && w.bn == kLdwBN) ? 1 : 0;
+            if (fm && k == 1) {  // dW1 with H0 recomputed from the features (and its relu mask)
+                if (!w.split || nd != 3) return set_err(DF_ERR_INVALID, "internal: H0-free sweep without the split dW1");
+                const WLayer& WL = P.wslayers[op.layer];
+                const WNet& WN = op.phase == TR_PHASE_T ? WL.t : WL.s;
+                const DevStage& S0 = P.wsstages[WN.stage0];
+                w.xb = nullptr;
+                w.feat = fbuf(op);
+                w.w0s = static_cast<const uint8_t*>(c->d_wsblob) + S0.src_off;
+                w.b0 = static_cast<const float*>(c->d_wbias) + WN.b0;
+                w.hmask = t->d_hmask;
+            }
             out.push_back(w);
         }
         return DF_OK;
@@ -673,6 +722,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         const LDenseArgs b = base_args(op);
         const bool keep = keeps(op);
         const bool fused = fused_front(op);
+        if (fm && !fused) return set_err(DF_ERR_INVALID, "internal: H0-free sweep without the fused front");
         // σ' argument of Dense k's output: H_k, or the stored σ'(x_k)
         auto DACT = [&](int k, LDenseArgs& a) {
             a.hprev = N.pre ? t->d_lv[k] : Hbuf(op, k);
@@ -683,7 +733,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
             LDenseArgs a = b;
             a.act = N.dn[k].act;
             if (k + 1 < nd && keep) {
-                if (k == 0) {
+                if (k == 0 && !fm) {  // (fmode: the inverse pass kept the features)
                     a.xsave = t->d_lx;
                     e = e == hipSuccess ? launch_gather_features(a, 16 * N.dn[0].bwd.mt, st) : e;
                 }
@@ -707,6 +757,13 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
                 dense(N.dn[k].fwd, LIN_BUF, LEPI_COUPLE, a);
             }
         }
+        // dW products of this net (launched after the backward; fmode: the split dW1 first,
+        // it writes the H0 relu mask the W1ᵀδ1 epilogue reads)
+        std::vector<LdwArgs> jobs;
+        {
+            const int rc0 = dw_args(op, par, jobs);
+            if (rc0 != DF_OK) return rc0;
+        }
         // backward: δ_{k-1} = (W_kᵀ δ_k) ⊙ σ'(H_{k-1}); x̄ = W0ᵀ δ_0 → z̄ (identity dims)
         const float* gcur = ybuf(par);
         if (fused) {
@@ -720,10 +777,22 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
                 if (e == hipSuccess) e = launch_couple_bwd(ht, mto, a, dgrid, lds, st);
             }
             gcur = dbuf(op, nd - 2, par);
+            if (fm) {
+                for (auto it = jobs.begin(); it != jobs.end(); ++it)
+                    if (it->feat) {
+                        if (e == hipSuccess) e = launch_ldw(*it, (unsigned)t->lgrid, st);
+                        jobs.erase(it);
+                        break;
+                    }
+            }
             for (int k = nd - 2; k >= 1; --k) {
                 LDenseArgs c2 = b;
                 c2.in = gcur;
                 DACT(k - 1, c2);
+                if (fm && k == 1) {  // σ'(H0) from the mask the split dW1 just wrote
+                    c2.hprev = nullptr;
+                    c2.hmask = t->d_hmask;
+                }
                 c2.out = dbuf(op, k - 1, par);
                 if (k == 1) {
                     c2.w0t = lb + N.dn[0].bwd.frag;
@@ -773,9 +842,6 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         // dW products of this net, merged with the next net's front when that net is the
         // next op and runs the fused front (its front reads only z̄ after this net's
         // W1ᵀδ1 kernel, the kept H, and writes the other parity's ȳ / δ_last)
-        std::vector<LdwArgs> jobs;
-        int rc = dw_args(op, par, jobs);
-        if (rc != DF_OK) return rc;
         front_done = false;
         // the split 256×256 dW runs as its own launch (one wave per SIMD, ldw_split_kernel)
         for (auto it = jobs.begin(); it != jobs.end();) {
@@ -913,7 +979,11 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
         }
         t->lgrid = std::max(1, c->n_cu);
         t->grid = t->lgrid;  // partial rows
+        t->fmode = fmode_eligible(t);
     }
+    if (const char* dbg = std::getenv("DF_TRAIN_DEBUG"); dbg && dbg[0] == '1')  // diagnostic: the sweep's form
+        std::fprintf(stderr, "[df] trainer: %s%s\n", t->layerwise ? "layer-wise" : "fused",
+                     t->layerwise ? (t->fmode ? ", H0-free sweep (features + H1 kept)" : ", H0/H1 kept or recomputed") : "");
     const size_t pb = sizeof(float) * (size_t)std::max<int64_t>(t->P, 4);
     if (hipMalloc(reinterpret_cast<void**>(&t->d_params), pb) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&t->d_m), pb) != hipSuccess ||
@@ -1025,8 +1095,10 @@ int df_train_gradient(df_train* t, const float* x, const float* theta_raw, int64
     if (rc != DF_OK) return rc;
 
     // 1. inverse pass keeping every layer's output (U[li] = snap[li], U[0] = z)
+    const bool fm = t->fmode && t->hsave_on && t->d_fsave;  // H0-free sweep (features + H1 kept)
     rc = run(c, MODE_LOGPDF, flow, x, theta_raw, nullptr, nullptr, nullptr, logpdf_sum ? logpdf_sum : t->d_lpsum,
-             batch, stream, t->d_snap, t->hsave_on ? t->d_hsave : nullptr, t->lwidth, t->lmax_h);
+             batch, stream, t->d_snap, t->hsave_on ? t->d_hsave : nullptr, t->lwidth, fm ? 1 : t->lmax_h,
+             fm ? t->d_fsave : nullptr);
     if (rc != DF_OK) return rc;
     const int64_t bd = batch * P.d;
     // 2. z̄ = z / N

@@ -454,7 +454,8 @@ __device__ __forceinline__ void snapshot(const f32x4 (&h)[TT][16], float* dst, c
 template <int TT>
 __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N, const int32_t* sfeat,
                                                const float* state, const int (&ro)[TT], WStager& sg,
-                                               f32x4 (&out)[TT][2], float* hs, const int64_t (&gs)[TT]) {
+                                               f32x4 (&out)[TT][2], float* hs, float* hs1, float* fs,
+                                               const int64_t (&gs)[TT]) {
     const int lane = threadIdx.x & 63, g = lane >> 4;
     f32x4 h[TT][16], acc[TT][16], lo[TT][16];
 
@@ -475,6 +476,11 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
 #pragma unroll
                 for (int e = 0; e < 8; ++e) v[e] = state[ro[t] + sfeat[32 * c + 8 * g + e]];
                 split8(v, x[t][0], x[t][1], x[t][2]);
+                if (fs && c == 0 && gs[t] >= 0) {  // training: the features (H0 is recomputed from them)
+                    float* fp = fs + gs[t] * 32 + 8 * g;
+                    __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f32x4*>(fp));
+                    __builtin_nontemporal_store(f32x4{v[4], v[5], v[6], v[7]}, reinterpret_cast<f32x4*>(fp + 4));
+                }
             }
             ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(N.stage0 + kWideSplitHalves * c, sg, a);
             split_chunk<TT, 16 / kWideSplitHalves, false, 16, 0>(sg.buf() + lane * 16, x, acc, acc, sg);
@@ -524,7 +530,6 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
 
     // ---- output Dense (<= 32 outputs) ----
     ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(N.stage0 + N.nst0 + 8 * kWideSplitHalves, sg, a);
-    float* const hs1 = hs ? hs + a.batch * a.hsave_w : nullptr;  // training: keep H1
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
         const f32x4 b = m < N.mto ? bias4(a.wbias + N.bo, m) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -691,8 +696,20 @@ __global__ void __launch_bounds__(SPLIT ? wide::kSplitWaves * 64 : wide::kThread
                 constexpr int PH = decltype(ph_tag)::value;
                 f32x4 out[TT][2];
                 float sum[TT];
-                if constexpr (SPLIT) eval_net_split<TT>(a, N, tab + L.pad0, state, ro, sg, out, hs, gs);
-                else eval_net(a, N, feat, state, ro, sg, out, hs, gs);
+                if constexpr (SPLIT) {
+                    // training snapshots: H0 and H1 at hs (hsave_h = 2), or with fsave the
+                    // features and H1 only (hs is then the net's H1 slot, hsave_h = 1)
+                    float* fs = nullptr;
+                    if (hs && a.fsave) {
+                        const int64_t slot = (hs - a.hsave) / (a.batch * a.hsave_w);
+                        fs = a.fsave + slot * a.batch * 32;
+                    }
+                    float* h0 = (hs && !a.fsave) ? hs : nullptr;
+                    float* h1 = hs ? (a.fsave ? hs : hs + a.batch * a.hsave_w) : nullptr;
+                    eval_net_split<TT>(a, N, tab + L.pad0, state, ro, sg, out, h0, h1, fs, gs);
+                } else {
+                    eval_net(a, N, feat, state, ro, sg, out, hs, gs);
+                }
                 couple<PH, TT>(out, L, tab, state, ro, sum);
 #pragma unroll
                 for (int t = 0; t < TT; ++t) {

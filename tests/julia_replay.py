@@ -415,6 +415,8 @@ def copy_trainables_bang(model, p):
     for D, name in _flux_trainables_arrays(model):
         a = getattr(D, name)
         n = a.size
+        if off + n > len(p):  # copyto! past the end of p: Julia's BoundsError
+            raise IndexError(f"copyto!: {n} elements from offset {off + 1} of a vector of length {len(p)}")
         setattr(D, name, p[off:off + n].reshape(a.shape, order="F").copy())
         off += n
     if off != len(p):

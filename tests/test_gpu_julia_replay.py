@@ -107,7 +107,8 @@ def test_julia_sample_train_sample_sequence(cuda):
         np.testing.assert_allclose(flow.valid_loss, vl, rtol=2e-4)
         dp = np.abs(c.params - p_ref)
         print("param |Δ| median / p99 / max", np.median(dp), np.quantile(dp, 0.99), dp.max())
-        assert np.quantile(dp, 0.99) <= 2e-5 and dp.max() <= 2 * EPOCHS * n_batches * 1e-3
+        # measured on the GPU: median 0, p99 3.0e-8, max 6.0e-8 (gpurun_out/r05a)
+        assert np.quantile(dp, 0.99) <= 2e-6 and dp.max() <= 1e-5
 
         # the Python mirror's train_ (θ raw, normalised in the kernels with the bounds) on
         # the same data gives bitwise the same parameters and losses
@@ -148,8 +149,10 @@ def test_julia_sample_train_sample_sequence(cuda):
             np.testing.assert_array_equal(lza, lzb)
         finally:
             c_new.finalize()
-        with pytest.raises(AssertionError):                  # DimensionMismatch on a short vector
+        with pytest.raises(IndexError):                      # copyto! past the end (BoundsError)
             J.copy_trainables_bang(chain_new, c.params[:-1])
+        with pytest.raises(AssertionError):                  # DimensionMismatch: a longer vector
+            J.copy_trainables_bang(chain_new, np.concatenate([c.params, np.zeros(1, np.float32)]))
 
         # 4. the model-level calls the shim exposes, θ as given, bounds still set
         x_va, th_va = data.validation_data()

@@ -222,6 +222,27 @@ def test_merged_sweep_bitwise_equals_separate_launches(cuda, monkeypatch, name, 
     assert out[0][1] == out[1][1]
 
 
+@pytest.mark.parametrize("B", [5, 300, 777, 3001])
+def test_h0_free_sweep_bitwise_equals_kept_h0(cuda, monkeypatch, capfd, B):
+    """Config-5 nets (wide SPLIT inverse, relu hidden-256): the default sweep keeps the
+    features and H1 only and recomputes H0 inside the split dW1 (with its relu mask for
+    the W1ᵀδ1 epilogue).  The recompute is the inverse pass's own first-Dense
+    arithmetic, so the gradient and Σ logpdf are bitwise those of the sweep that keeps
+    H0 (DF_TRAIN_H0=1); batches below / across the 32-sample dW steps included."""
+    spec, chain, d, n = _setup("cfg5")
+    x, th = _inputs(d, n, B)
+    out = []
+    monkeypatch.setenv("DF_TRAIN_DEBUG", "1")
+    for keep_h0 in ("0", "1"):
+        monkeypatch.setenv("DF_TRAIN_H0", keep_h0)
+        tr = HIPTrainer(spec_to_element(spec).hip(), Adam())
+        err = capfd.readouterr().err
+        assert ("H0-free sweep" in err) == (keep_h0 == "0"), err
+        out.append(_gpu_grad(tr, x, th, cuda))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
+
+
 @pytest.mark.parametrize("name", ["cfg2", "wide"])
 def test_gradient_bitwise_reproducible(cuda, path, name):
     spec, chain, d, n = _setup(name)
