@@ -88,8 +88,8 @@ struct LDenseArgs {
     const uint8_t* w0t;
     int w0t_mt, w0t_nkq;
     const uint8_t* w0s;     // SPLIT instances: W0ᵀ as bf16x3 planes [c][m][p][lane][8] (x̄ on bf16 MFMA), or nullptr
-    const uint32_t* hmask;  // LEPI_DACT(_XBAR), relu: σ'(H) from a relu mask [B][8] words (16 bits per m-tile:
-                            // bit j of m-tile m ↔ row 16m + j; written by the H0-recomputing split dW1), else hprev
+    const uint32_t* hmask;  // LEPI_DACT(_XBAR), relu: σ'(H) from the relu mask of the H0-recomputing split
+                            // dW1 (LdwArgs::hmask), else hprev
     // couple_bwd_kernel: second product W_outᵀ ȳ (fragments [kq][m][lane][4], m < 16·HT rows)
     const uint8_t* w2frag;
     int nkq2;
@@ -115,7 +115,10 @@ struct LdwArgs {
     const float* feat;
     const uint8_t* w0s;
     const float* b0;
-    uint32_t* hmask;        // [B][8]: 16 bits per m-tile m, bit j ↔ H0 row 16m + j > 0
+    // relu mask of H0, blocks of 256 dwords per aligned 32-sample step S (= s >> 5): block S,
+    // dword (S·4 + w)·64 + 16g' + j, bit 4(2mm + tt) + r ↔ H0 row 16(4w + mm) + j > 0 of
+    // sample 32S + 16tt + 4g' + r (the lane (g', j) of wave w that computed it)
+    uint32_t* hmask;
 };
 
 // One merged launch: up to three non-split dW products (ldw) of net i and, optionally, the

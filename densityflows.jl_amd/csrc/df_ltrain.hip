@@ -1,4 +1,6 @@
 // df_ltrain.hip — kernels of the layer-wise training path (df_ltrain.h).
+#include <utility>
+
 #include "df_chain_impl.h"
 #include "df_ltrain.h"
 #include "df_train_impl.h"
@@ -231,19 +233,22 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
                 // sample reads the last row; its δ is zeroed and never stored)
                 const int64_t s = valid[t] ? smp[t] : a.batch - 1;
                 if (a.hmask) {  // relu σ' from the mask of the H0-recomputing split dW1 (no H read)
-                    uint32_t mk[8];
-                    {
-                        const uint4* mp = reinterpret_cast<const uint4*>(a.hmask + s * 8);
-                        const uint4 u0 = mp[0], u1 = mp[1];
-                        mk[0] = u0.x; mk[1] = u0.y; mk[2] = u0.z; mk[3] = u0.w;
-                        mk[4] = u1.x; mk[5] = u1.y; mk[6] = u1.z; mk[7] = u1.w;
-                    }
+                    // sample s = 32S + 16tt + 4g' + r: rows 16(4w + mm) + 4g + q in dwords
+                    // (S·4 + w)·64 + 16g' + 4g + q, bit 4(2mm + tt) + r (df_ltrain.h LdwArgs::hmask)
+                    const int sl = (int)(s & 31);
+                    const int sh = 4 * ((sl >> 4) & 1) + (sl & 3);
+                    const uint32_t* mb = a.hmask + (s >> 5) * 256 + 16 * ((sl >> 2) & 3) + 4 * g;
+                    uint4 mq[4];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) mq[w] = *reinterpret_cast<const uint4*>(mb + 64 * w);
 #pragma unroll
                     for (int m = 0; m < MT; ++m) {
                         f32x4 v = acc[t][m];
-                        const uint32_t bits = mk[m >> 1] >> (16 * (m & 1) + 4 * g);
+                        const uint4 u = mq[m >> 2];
+                        const int b = 8 * (m & 3) + sh;
+                        const uint32_t qb[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) v[q] = ((bits >> q) & 1u) ? v[q] : 0.f;
+                        for (int q = 0; q < 4; ++q) v[q] = ((qb[q] >> b) & 1u) ? v[q] : 0.f;
                         if (!valid[t]) v = f32x4{0.f, 0.f, 0.f, 0.f};
                         else *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + 16 * m + 4 * g) = v;
                         if constexpr (EPI == LEPI_DACT_XBAR) acc[t][m] = v;  // δ0 → B operand of W0ᵀ
@@ -701,6 +706,15 @@ __device__ __forceinline__ void ldw_body(const LdwArgs& a, float* lsm, int bid, 
 #ifndef DF_LDW_H0_HALVES
 #define DF_LDW_H0_HALVES 0
 #endif
+// compile-time loop: f(std::integral_constant<int, i>) for i < N
+template <class F, int... I>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
 #if DF_LDW_DMA
 __device__ __forceinline__ int ldw_slot(int row, int sg) { return sg ^ ((-(row >> 2)) & 3); }
 
@@ -726,7 +740,9 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
     const int m0 = 8 * (wave & 1), n0 = 8 * (wave >> 1);
     const int q = lane, sg = wave;  // this thread's staging item of each operand: rows 4q.., samples 8sg..
     const int nblk = gridDim.x;
-    const int64_t per = (a.batch + nblk - 1) / nblk;
+    // sample range of a workgroup: a multiple of the 32-sample step (steps are aligned blocks
+    // of the batch, which the H0R relu-mask layout indexes by)
+    const int64_t per = ((a.batch + nblk - 1) / nblk + 31) / 32 * 32;
     const int64_t s_begin = (int64_t)blockIdx.x * per;
     const int64_t s_end = (s_begin + per < a.batch) ? s_begin + per : a.batch;
 
@@ -796,17 +812,16 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
                                 fr[tt][1][0], fr[tt][1][1], fr[tt][1][2], fr[tt][1][3]};
             uni::split8(v, x[tt][0], x[tt][1], x[tt][2]);
         }
-        // mask word of this lane: sample sl = lane & 31 of the step, m-tiles 4w + 2mp, + 1
-        const int sl = lane & 31, mp = lane >> 5;
-        uint32_t mword = 0u;
-#pragma unroll
-        for (int mp2 = 0; mp2 < 2; ++mp2) {
-#pragma unroll
-            for (int tt = 0; tt < 2; ++tt) {
+        const bool full = s0 + 32 <= s_end;  // (uniform) no sample of the step past the range
+        uint32_t mv = 0u;                    // this lane's dword of the wave's relu-mask block
+        // (compile-time loops: the mask's v_writelane takes its lane as an inline constant)
+        sfor<2>([&](auto mp2c) {
+            constexpr int mp2 = decltype(mp2c)::value;
+            sfor<2>([&](auto ttc) {
+                constexpr int tt = decltype(ttc)::value;
                 float hv[8];  // rows 16(4w + 2mp2 + hh) + j, samples 16tt + 4g + r: hv[4hh + r]
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const int mm = 2 * mp2 + hh;
+                sfor<2>([&](auto hhc) {
+                    constexpr int hh = decltype(hhc)::value, mm = 2 * mp2 + hh;
                     f32x4 v = f32x4{w0.b[mm], w0.b[mm], w0.b[mm], w0.b[mm]};
                     v = uni::mfma_bf(x[tt][0], w0.w[mm][2], v);
                     v = uni::mfma_bf(x[tt][1], w0.w[mm][1], v);
@@ -815,16 +830,16 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
                     v = uni::mfma_bf(x[tt][1], w0.w[mm][0], v);
                     v = uni::mfma_bf(x[tt][0], w0.w[mm][0], v);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const bool ok = s0 + 16 * tt + 4 * g + r < s_end;
-                        const float h = ok ? uni::relu_fast(v[r]) : 0.f;
-                        hv[4 * hh + r] = h;
-                        // lane group g' of the ballot: rows 16mt + 0..15 of sample 16tt + 4g' + r
-                        const uint64_t bal = __ballot(h > 0.f);
-                        if ((sl >> 4) == tt && (sl & 3) == r && mp == mp2)
-                            mword |= (uint32_t)((bal >> (16 * ((sl >> 2) & 3))) & 0xffffu) << (16 * hh);
+                    for (int r = 0; r < 4; ++r) hv[4 * hh + r] = uni::relu_fast(v[r]);
+                    if (!full) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (s0 + 16 * tt + 4 * g + r >= s_end) hv[4 * hh + r] = 0.f;
                     }
-                }
+                    // relu mask (hmask layout): bit 4(2mm + tt) + r of this lane's dword
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) mv |= (hv[4 * hh + r] > 0.f ? 1u : 0u) << (4 * (2 * mm + tt) + r);
+                });
                 uni::bf16x8 p[3];
                 uni::split8(hv, p[0], p[1], p[2]);
                 const int sgp = 2 * tt + (g >> 1);  // 8-sample group of samples 16tt + 4g ..
@@ -839,10 +854,11 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
                         *reinterpret_cast<uint64_t*>(dst + k * PB) = u[hh];
                     }
                 }
-            }
-        }
-        const int64_t s = s0 + sl;
-        if (s < s_end) reinterpret_cast<uint32_t*>(a.hmask)[s * 8 + 2 * wave + mp] = mword;
+            });
+        });
+        // the step's 32 samples are one aligned block of the batch (the sample range of a
+        // workgroup is a multiple of 32): mask block (s0 / 32, wave), one dword a lane
+        a.hmask[((s0 >> 5) * 4 + wave) * 64 + lane] = mv;
     };
     // step 2 for one operand: rows 4q + i, samples 8sg + e
     // Rows q + 64i (not 4q + i): the 16 lanes of a plane write then cover all 16

@@ -147,7 +147,7 @@ struct df_train {
     // H0-free sweep (round 5; wide SPLIT chains of relu hidden-256 nets, DF_TRAIN_H0=1 turns it
     // off): the inverse pass keeps each net's features vcat(θ, u)[axis_nn] ([layer·2 + net][B][32])
     // and H1 only (d_hsave with one slot per net); the split dW1 recomputes H0 from the
-    // features and writes its relu mask (d_hmask, [B][8] words) for the W1ᵀδ1 epilogue
+    // features and writes its relu mask (d_hmask, 1 KiB per 32 samples) for the W1ᵀδ1 epilogue
     bool fmode = false;
     float* d_fsave = nullptr;
     uint32_t* d_hmask = nullptr;
@@ -507,7 +507,7 @@ int ensure_capacity(df_train* t, int64_t batch) {
                 hipMalloc(reinterpret_cast<void**>(&t->d_hsave), hbytes) == hipSuccess) {
                 t->hsave_on = true;
                 if (t->fmode && (hipMalloc(reinterpret_cast<void**>(&t->d_fsave), fbytes) != hipSuccess ||
-                                 hipMalloc(reinterpret_cast<void**>(&t->d_hmask), (size_t)cap * 32) != hipSuccess))
+                                 hipMalloc(reinterpret_cast<void**>(&t->d_hmask), (size_t)(cap + 31) / 32 * 1024) != hipSuccess))
                     return set_err(DF_ERR_NOMEM, "hipMalloc failed (training feature snapshots)");
             }
             (void)hipGetLastError();
