@@ -25,7 +25,8 @@
 namespace df {
 
 enum : int { LIN_BUF = 0, LIN_GATHER = 1 };
-enum : int { LEPI_ACT = 0, LEPI_COUPLE = 1, LEPI_DACT = 2, LEPI_XBAR = 3, LEPI_DACT_XBAR = 4 };
+enum : int { LEPI_ACT = 0, LEPI_COUPLE = 1, LEPI_DACT = 2, LEPI_XBAR = 3, LEPI_DACT_XBAR = 4,
+             LEPI_DACT_XBAR_MASK = 5 };  // (5: SPLIT only, σ' from LDenseArgs::hmask)
 
 constexpr int kLChunkBytes = 32 * 1024;  // weight chunk (LDS, double-buffered)
 #ifndef DF_LTILES

@@ -12,6 +12,24 @@ namespace {
 using impl::lds4;
 using impl::mfma4;
 
+// 8 values (two f32x4 of a lane, a then b) → their bf16x3 planes on the VALU (uni::split8:
+// v_mov + v_dot2c per remainder).  DF_LT_MREM=1: the remainders on the matrix pipe
+// (uni::split8_mrem, one v_mfma_f32_16x16x16_bf16 with A = −I per 4 values: an exact
+// element-wise x − hi for any 4 values of a lane), bitwise the same planes; measured slower
+// here (config-5 step 34.2 vs 33.4 ms, gpurun_out/r05m)
+#ifndef DF_LT_MREM
+#define DF_LT_MREM 0
+#endif
+__device__ __forceinline__ void split8x(const f32x4& a, const f32x4& b, uni::bf16x8& p0, uni::bf16x8& p1,
+                                        uni::bf16x8& p2) {
+    if constexpr (DF_LT_MREM) {
+        uni::split8_mrem(uni::neg_eye(), a, b, p0, p1, p2);
+    } else {
+        const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        uni::split8(v, p0, p1, p2);
+    }
+}
+
 __device__ __forceinline__ float gather_feature(const LDenseArgs& a, int slot, int64_t s) {
     if (slot < a.n) {
         float v = a.theta[s * a.n + slot];
@@ -40,6 +58,10 @@ template <int MT, int IN, int EPI, bool SPLIT = false, int NW = kWavesPerBlock, 
 __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int T = TT;
+    // LEPI_DACT_XBAR_MASK: LEPI_DACT_XBAR with σ'(H0) from the split dW1's relu mask
+    // (a.hmask) — no σ' argument rows are loaded, so none are held in registers
+    constexpr bool XB = (EPI == LEPI_DACT_XBAR || EPI == LEPI_DACT_XBAR_MASK);
+    constexpr bool MASK = (EPI == LEPI_DACT_XBAR_MASK);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, j = lane & 15;
     const int chunk_bytes = SPLIT ? MT * 3072 : a.chunk_kq * MT * 1024;
@@ -69,7 +91,7 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
     };
     // after the chunk buffer(s): two full chunks, or the single (possibly short) one
     uint8_t* w0t_lds = smem + (nchunks > 1 ? 2 * chunk_bytes : SPLIT ? chunk_bytes : a.nkq * MT * 1024);
-    if constexpr (EPI == LEPI_DACT_XBAR) {  // W0ᵀ fragments stay resident for the x̄ product
+    if constexpr (XB) {  // W0ᵀ fragments stay resident for the x̄ product
         // f32 fragments, or (SPLIT, a.w0s) bf16x3 planes [c][m][p][lane][8] of 32-row chunks
         const int n16 = (SPLIT && a.w0s) ? (a.w0t_nkq / 2) * a.w0t_mt * 3 * 64 : a.w0t_mt * a.w0t_nkq * 64;
         const f32x4* src = reinterpret_cast<const f32x4*>((SPLIT && a.w0s) ? a.w0s : a.w0t);
@@ -83,7 +105,7 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
         }
     }
     dma(0, smem);
-    if (nchunks == 1 || EPI == LEPI_DACT_XBAR) {
+    if (nchunks == 1 || XB) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
@@ -124,7 +146,7 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
         load_x(0, xn);  // prefetched one k-quad ahead
         // DACT epilogues: tile 0's first σ' arguments are loaded during the last k-quad
         // (the epilogues of all waves otherwise hit HBM in one burst)
-        constexpr bool kDact = (EPI == LEPI_DACT || EPI == LEPI_DACT_XBAR);
+        constexpr bool kDact = (EPI == LEPI_DACT || XB) && !MASK;  // σ' rows prefetched
         constexpr int HR = (MT < 8 ? MT : 8) / (T > 2 ? 2 : 1);  // σ' arguments in flight
         const int64_t s0h = valid[0] ? smp[0] : a.batch - 1;
         f32x4 h0[kDact ? HR : 1];
@@ -141,17 +163,13 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
                 }
                 uni::bf16x8 xp[T][3];
 #pragma unroll
-                for (int t = 0; t < T; ++t) {
-                    const float v[8] = {xn[t][0],  xn[t][1],  xn[t][2],  xn[t][3],
-                                        xn1[t][0], xn1[t][1], xn1[t][2], xn1[t][3]};
-                    uni::split8(v, xp[t][0], xp[t][1], xp[t][2]);
-                }
+                for (int t = 0; t < T; ++t) split8x(xn[t], xn1[t], xp[t][0], xp[t][1], xp[t][2]);
                 if (c + 1 < nchunks) {
                     load_x(2 * c + 2, xn);
                     load_x(2 * c + 3, xn1);
                 }
                 if constexpr (kDact) {
-                    if (c + 1 == nchunks && !a.hmask) {
+                    if (c + 1 == nchunks) {
 #pragma unroll
                         for (int m = 0; m < HR; ++m)
                             h0[m] = *reinterpret_cast<const f32x4*>(a.hprev + s0h * a.ld_h + 4 * g + 16 * m);
@@ -217,7 +235,7 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
         }
 
         // ---- epilogue: rows 16m + 4g + q of sample smp[t] ----
-        if constexpr (EPI == LEPI_DACT || EPI == LEPI_DACT_XBAR) {
+        if constexpr (EPI == LEPI_DACT || XB) {
 #if DF_LDENSE_DIAG == 1  // timing diagnostic (wrong results): δ stored without σ' or x̄
 #pragma unroll
             for (int t = 0; t < T; ++t)
@@ -232,7 +250,7 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
                 // the σ' arguments of the whole tile are loaded at once (a padding
                 // sample reads the last row; its δ is zeroed and never stored)
                 const int64_t s = valid[t] ? smp[t] : a.batch - 1;
-                if (a.hmask) {  // relu σ' from the mask of the H0-recomputing split dW1 (no H read)
+                if constexpr (MASK) {  // relu σ' from the mask of the H0-recomputing split dW1 (no H read)
                     // sample s = 32S + 16tt + 4g' + r: rows 16(4w + mm) + 4g + q in dwords
                     // (S·4 + w)·64 + 16g' + 4g + q, bit 4(2mm + tt) + r (df_ltrain.h LdwArgs::hmask)
                     const int sl = (int)(s & 31);
@@ -251,7 +269,7 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
                         for (int q = 0; q < 4; ++q) v[q] = ((qb[q] >> b) & 1u) ? v[q] : 0.f;
                         if (!valid[t]) v = f32x4{0.f, 0.f, 0.f, 0.f};
                         else *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + 16 * m + 4 * g) = v;
-                        if constexpr (EPI == LEPI_DACT_XBAR) acc[t][m] = v;  // δ0 → B operand of W0ᵀ
+                        if constexpr (XB) acc[t][m] = v;  // δ0 → B operand of W0ᵀ
                     }
                 } else {
                 const float* hrow = a.hprev + s * a.ld_h + 4 * g;
@@ -272,10 +290,10 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
                     }
                     if (!valid[t]) v = f32x4{0.f, 0.f, 0.f, 0.f};
                     else *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + 16 * m + 4 * g) = v;
-                    if constexpr (EPI == LEPI_DACT_XBAR) acc[t][m] = v;  // δ0 → B operand of W0ᵀ
+                    if constexpr (XB) acc[t][m] = v;  // δ0 → B operand of W0ᵀ
                 }
                 }
-                if constexpr (EPI == LEPI_DACT_XBAR) {
+                if constexpr (XB) {
                     // x̄ = W0ᵀ δ0 (rows = conditioner features, <= 4 tiles) → z̄ of identity dims
                     // The z̄ entries it adds to are read ahead of the product (their latency
                     // overlaps its MFMAs), all loads ahead of all stores: distinct features
@@ -304,11 +322,8 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
 #pragma unroll
                         for (int c = 0; c < MT / 2; ++c) {
                             if (2 * c < a.w0t_nkq) {
-                                const float v[8] = {acc[t][2 * c][0],     acc[t][2 * c][1],     acc[t][2 * c][2],
-                                                    acc[t][2 * c][3],     acc[t][2 * c + 1][0], acc[t][2 * c + 1][1],
-                                                    acc[t][2 * c + 1][2], acc[t][2 * c + 1][3]};
                                 uni::bf16x8 x0, x1, x2;
-                                uni::split8(v, x0, x1, x2);
+                                split8x(acc[t][2 * c], acc[t][2 * c + 1], x0, x1, x2);
 #pragma unroll
                                 for (int m = 0; m < 4; ++m) {
                                     if (m < a.w0t_mt) {
@@ -807,11 +822,7 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
     auto h0_compute = [&](int64_t s0, const f32x4 (&fr)[2][2], const W0In& w0) {
         uni::bf16x8 x[2][3];  // A operand: lane (g, i) holds features 8g + e of sample 16tt + i
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-            const float v[8] = {fr[tt][0][0], fr[tt][0][1], fr[tt][0][2], fr[tt][0][3],
-                                fr[tt][1][0], fr[tt][1][1], fr[tt][1][2], fr[tt][1][3]};
-            uni::split8(v, x[tt][0], x[tt][1], x[tt][2]);
-        }
+        for (int tt = 0; tt < 2; ++tt) split8x(fr[tt][0], fr[tt][1], x[tt][0], x[tt][1], x[tt][2]);
         const bool full = s0 + 32 <= s_end;  // (uniform) no sample of the step past the range
         uint32_t mv = 0u;                    // this lane's dword of the wave's relu-mask block
         // (compile-time loops: the mask's v_writelane takes its lane as an inline constant)
@@ -841,7 +852,7 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
                     for (int r = 0; r < 4; ++r) mv |= (hv[4 * hh + r] > 0.f ? 1u : 0u) << (4 * (2 * mm + tt) + r);
                 });
                 uni::bf16x8 p[3];
-                uni::split8(hv, p[0], p[1], p[2]);
+                split8x(f32x4{hv[0], hv[1], hv[2], hv[3]}, f32x4{hv[4], hv[5], hv[6], hv[7]}, p[0], p[1], p[2]);
                 const int sgp = 2 * tt + (g >> 1);  // 8-sample group of samples 16tt + 4g ..
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
@@ -879,7 +890,7 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
         for (int i = 0; i < 4; ++i) {
             const float(&v)[8] = x[i];
             uni::bf16x8 p0, p1, p2;
-            uni::split8(v, p0, p1, p2);
+            split8x(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, p0, p1, p2);
             const int row = q + 64 * i;
             uint8_t* dst = T + row * 64 + 16 * ldw_slot(row, sg);
             *reinterpret_cast<uni::bf16x8*>(dst) = p0;
@@ -1181,6 +1192,9 @@ void* ldense_ptr(int mt, int in_kind, int epi, bool split = false) {
             return reinterpret_cast<void*>(&ldense_kernel<16, LIN_BUF, LEPI_DACT, true, kSplitWaves, kSplitTiles>);
         if (epi == LEPI_DACT_XBAR)
             return reinterpret_cast<void*>(&ldense_kernel<16, LIN_BUF, LEPI_DACT_XBAR, true, kSplitWaves, kSplitTiles>);
+        if (epi == LEPI_DACT_XBAR_MASK)
+            return reinterpret_cast<void*>(
+                &ldense_kernel<16, LIN_BUF, LEPI_DACT_XBAR_MASK, true, kSplitWaves, kSplitTiles>);
         return nullptr;
     }
     switch (mt) {
@@ -1222,7 +1236,7 @@ hipError_t set_ldense_lds_limit(size_t lds) {
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    for (int epi : {LEPI_DACT, LEPI_DACT_XBAR}) {
+    for (int epi : {LEPI_DACT, LEPI_DACT_XBAR, LEPI_DACT_XBAR_MASK}) {
         hipError_t e = hipFuncSetAttribute(ldense_ptr(16, LIN_BUF, epi, true),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

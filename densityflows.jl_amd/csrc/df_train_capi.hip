@@ -800,7 +800,9 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
                     c2.w0t_nkq = N.dn[0].bwd.nkq;
                     const LOp& lo = N.dn[k].bwd;
                     const int nchunks = (lo.nkq + lo.chunk_kq - 1) / lo.chunk_kq;
-                    c2.sfrag = sfrag_of(lo, LIN_BUF, LEPI_DACT_XBAR);
+                    const int xepi = (fm && k == 1) ? LEPI_DACT_XBAR_MASK : LEPI_DACT_XBAR;
+                    c2.sfrag = sfrag_of(lo, LIN_BUF, xepi);
+                    if (fm && !c2.sfrag) return set_err(DF_ERR_INVALID, "internal: H0-free sweep without the split W1ᵀδ1");
                     // x̄ on split products when the W1ᵀδ1 product is SPLIT and W0ᵀ has planes
                     c2.w0s = (c2.sfrag && N.dn[0].bwd.sfrag >= 0 && c2.w0t_nkq <= 16) ? lsb + N.dn[0].bwd.sfrag
                                                                                      : nullptr;
@@ -813,7 +815,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
                     c2.wfrag = lb + lo.frag;
                     c2.nkq = lo.nkq;
                     c2.chunk_kq = lo.chunk_kq;
-                    if (e == hipSuccess) e = launch_ldense(lo.mt, LIN_BUF, LEPI_DACT_XBAR, c2, dgrid, lds2, st);
+                    if (e == hipSuccess) e = launch_ldense(lo.mt, LIN_BUF, xepi, c2, dgrid, lds2, st);
                 } else {
                     dense(N.dn[k].bwd, LIN_BUF, LEPI_DACT, c2);
                 }

@@ -40,6 +40,12 @@ __device__ __forceinline__ const V& cref(const V* p) {
 #ifndef DF_WIDE_SBIAS
 #define DF_WIDE_SBIAS 0
 #endif
+// timing diagnostics of the SPLIT kernel (wrong results): bit 0 = no Dense epilogues
+// (relu / hi + lo), bit 1 = no activation splits (chunk 0's planes reused), bit 2 = no
+// stage waits / barriers
+#ifndef DF_WIDE_DIAG
+#define DF_WIDE_DIAG 0
+#endif
 // Bias rows 16m + 4g + r of lane group g: a vector load, or (DF_WIDE_SBIAS) 16
 // scalar-loaded floats selected per lane group.
 __device__ __forceinline__ f32x4 bias4(const float* b, int m) {
@@ -144,14 +150,14 @@ __device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
         for (int q = 1; q < NB - 1; ++q)
             if (nidx + q < sg.n) newer += dma_ops<NW>(cref(a.stages + cref(sg.sched + nidx + q)).bytes, wave);
         wait_vmcnt(newer);
-    } else {
+    } else if (!(DF_WIDE_DIAG & 4)) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     // A bare s_barrier: __syncthreads()'s release fence would also wait for the
     // newer stages' DMA (vmcnt(0)).  The stage ring is the only LDS data shared
     // between waves here, and each wave's reads of the slot being refilled have
     // returned (lgkmcnt(0)) before it arrives.
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (!(DF_WIDE_DIAG & 4)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     sg.idx = nidx;
     sg.cur = s;
     if (nidx >= sg.n || cref(sg.sched + nidx) != s) {  // off schedule (never produced by the planner)
@@ -434,6 +440,7 @@ __device__ __forceinline__ void split_tiles(const f32x4 (&h)[TT][16], int c, bf1
 #ifndef DF_WSNAP_SPREAD
 #define DF_WSNAP_SPREAD 1
 #endif
+
 // Training snapshot of a hidden activation (H0 or H1, rows of sample gs[t]) during
 // 32-input chunk c of the Dense that consumes it. SPREAD: the chunk's own two m-tiles
 // (its stores drain during the chunk's MFMAs; a stage switch waits vmcnt(0), so a
@@ -495,7 +502,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
 #pragma unroll
         for (int m = 0; m < 16; ++m)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) h[t][m][r] = uni::relu_fast(acc[t][m][r]);
+            for (int r = 0; r < 4; ++r) h[t][m][r] = (DF_WIDE_DIAG & 1) ? acc[t][0][r] : uni::relu_fast(acc[t][m][r]);
 
     // ---- hidden Dense 256×256 ----
 #pragma unroll
@@ -511,7 +518,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
     for (int c = 0; c < 8; ++c) {
         ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(N.stage0 + N.nst0 + kWideSplitHalves * c, sg, a);
         bf16x8 x[TT][3];
-        split_tiles<TT>(h, c, x);
+        split_tiles<TT>(h, (DF_WIDE_DIAG & 2) ? 0 : c, x);
         if (hs) snapshot<TT, DF_WSNAP_SPREAD != 0>(h, hs, gs, a.hsave_w, c);  // training: keep H0 (as in eval_net)
         split_chunk<TT, 16 / kWideSplitHalves, true, 16, 0>(sg.buf() + lane * 16, x, acc, lo, sg);
         if constexpr (kWideSplitHalves == 2) {
@@ -523,9 +530,9 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
     for (int t = 0; t < TT; ++t)
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
-            const f32x4 v = acc[t][m] + lo[t][m];
+            const f32x4 v = (DF_WIDE_DIAG & 1) ? acc[t][m & 1] : acc[t][m] + lo[t][m];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) h[t][m][r] = uni::relu_fast(v[r]);
+            for (int r = 0; r < 4; ++r) h[t][m][r] = (DF_WIDE_DIAG & 1) ? v[r] : uni::relu_fast(v[r]);
         }
 
     // ---- output Dense (<= 32 outputs) ----
@@ -545,7 +552,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
         if (N.nso == 2 && c == 4) ensure<kSplitWaves, DF_WIDE_STAGGER != 0, kWideSplitBufs>(so0 + 1, sg, a);
         const uint8_t* buf = sg.buf() + lane * 16;
         bf16x8 x[TT][3];
-        split_tiles<TT>(h, c, x);
+        split_tiles<TT>(h, (DF_WIDE_DIAG & 2) ? 0 : c, x);
         if (hs1) snapshot<TT, DF_WSNAP_SPREAD != 0>(h, hs1, gs, a.hsave_w, c);
         if (N.mto == 2) split_chunk<TT, 2, true>(buf + (c & (8 / N.nso - 1)) * 2 * 3072, x, acc, lo, sg);
         else split_chunk<TT, 1, true>(buf + c * 3072, x, acc, lo, sg);
