@@ -466,7 +466,44 @@ __device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, 
             hn[kq] = kq < a.nkq ? *reinterpret_cast<const f32x4*>(a.in + sl * a.ld_in + 16 * kq + 4 * g)
                                 : f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    if ((int64_t)bid * kWavesPerBlock + wave < ntiles) load_h((int64_t)bid * kWavesPerBlock + wave);
+    // the pullback's operands of rows 16m + 4g + q (transformed dims af[row]): the dims are
+    // fixed per lane (hoisted, one byte each; 0xff: no transformed dim), and z̄, u_out (s
+    // phases) or exp(−s) (t phases) of the next tile are loaded as soon as this tile's are
+    // consumed — no dependent global round trip inside the tile
+    uint32_t dimw[MTO];
+#pragma unroll
+    for (int m = 0; m < MTO; ++m) {
+        dimw[m] = 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = 16 * m + 4 * g + q;
+            dimw[m] |= (uint32_t)(row < a.n_af ? a.af[row] - a.n : 0xff) << (8 * q);
+        }
+    }
+    auto dimq = [&](int m, int q) { return (int)((dimw[m] >> (8 * q)) & 0xffu); };
+    float zbn[MTO][4], oun[MTO][4];
+    auto load_p = [&](int64_t tile) {
+        int64_t sl = tile * 16 + j;
+        sl = sl < a.batch ? sl : a.batch - 1;
+#pragma unroll
+        for (int m = 0; m < MTO; ++m)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int dim = dimq(m, q);
+                zbn[m][q] = dim != 0xff ? a.zbar[sl * a.d + dim] : 0.f;
+                oun[m][q] = dim == 0xff ? 0.f
+                            : sph  ? a.u_out[sl * a.d + dim]
+                            : rnvp ? a.ebuf[sl * 32 + 16 * m + 4 * g + q]
+                                   : 1.f;
+            }
+    };
+    // (MTO = 2: the operands of the tile itself, loaded at its pullback — the prefetch's
+    // registers would spill there)
+    constexpr bool PFP = (MTO == 1);
+    if ((int64_t)bid * kWavesPerBlock + wave < ntiles) {
+        load_h((int64_t)bid * kWavesPerBlock + wave);
+        if (PFP) load_p((int64_t)bid * kWavesPerBlock + wave);
+    }
     for (int64_t tile = (int64_t)bid * kWavesPerBlock + wave; tile < ntiles; tile += tstride) {
         const int64_t s = tile * 16 + j;
         const bool valid = s < a.batch;
@@ -489,6 +526,7 @@ __device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, 
             }
         }
         // σo(W_out h .+ b), then the coupling pullback (rrule(RNVP_backward) RNVP.jl:133-139)
+        if (!PFP) load_p(tile);
         f32x4 dy[MTO];
 #pragma unroll
         for (int m = 0; m < MTO; ++m) {
@@ -504,14 +542,14 @@ __device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, 
             for (int q = 0; q < 4; ++q) {
                 const int row = row0 + q;
                 if (valid && row < a.n_af) {
-                    const int dim = a.af[row] - a.n;
-                    const float zb = a.zbar[s * a.d + dim];
+                    const int dim = dimq(m, q);
+                    const float zb = zbn[m][q];
                     float dq;
                     if (sph) {
                         a.ebuf[s * 32 + row] = expf(-v[q]);
-                        dq = -zb * a.u_out[s * a.d + dim] + a.inv_n;  // s̄ = -z̄_af·z_af - j̄
+                        dq = -zb * oun[m][q] + a.inv_n;                 // s̄ = -z̄_af·z_af - j̄
                     } else {
-                        const float e = rnvp ? a.ebuf[s * 32 + row] : 1.f;
+                        const float e = oun[m][q];                     // exp(-s) (RNVP) or 1 (NICE)
                         dq = -zb * e;                                   // t̄ = -z̄_af·exp(-s)
                         if (rnvp) a.zbar[s * a.d + dim] = zb * e;       // ū_af = z̄_af·exp(-s)
                     }
@@ -521,33 +559,40 @@ __device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, 
             }
             if (valid) *reinterpret_cast<f32x4*>(a.out + s * a.ld_out + row0) = dy[m];
         }
-        // δ = (W_outᵀ ȳ) ⊙ σ'(h)
-        f32x4 acc[HT];
+        if (PFP && tile + tstride < ntiles) load_p(tile + tstride);  // this tile's operands consumed
+        // δ = (W_outᵀ ȳ) ⊙ σ'(h), one 16-row tile at a time (its product, σ' and store: 4
+        // accumulator registers live instead of 4·HT)
+        constexpr int MB = 1;
 #pragma unroll
-        for (int m = 0; m < HT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int m0 = 0; m0 < HT; m0 += MB) {
+            f32x4 acc[MB];
 #pragma unroll
-        for (int kq = 0; kq < MTO; ++kq) {
-            if (kq < a.nkq2) {
+            for (int mb = 0; mb < MB; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int m = 0; m < HT; ++m) {
-                    const f32x4 w = lds4(wt + (kq * HT + m) * 1024 + lane * 16);
+            for (int kq = 0; kq < MTO; ++kq) {
+                if (kq < a.nkq2) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) acc[m] = mfma4(w[q], dy[kq][q], acc[m]);
+                    for (int mb = 0; mb < MB; ++mb) {
+                        const f32x4 w = lds4(wt + (kq * HT + m0 + mb) * 1024 + lane * 16);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) acc[mb] = mfma4(w[q], dy[kq][q], acc[mb]);
+                    }
                 }
             }
-        }
-        if (valid) {
+            if (valid) {
 #pragma unroll
-            for (int m = 0; m < HT; ++m) {
-                f32x4 v = acc[m];
-                if (a.dact == DF_ACT_RELU) {
+                for (int mb = 0; mb < MB; ++mb) {
+                    const int m = m0 + mb;
+                    f32x4 v = acc[mb];
+                    if (a.dact == DF_ACT_RELU) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) v[q] = (h[m][q] > 0.f) ? v[q] : 0.f;
-                } else if (a.dact != DF_ACT_IDENTITY) {
+                        for (int q = 0; q < 4; ++q) v[q] = (h[m][q] > 0.f) ? v[q] : 0.f;
+                    } else if (a.dact != DF_ACT_IDENTITY) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) v[q] = v[q] * trn::act_grad(a.dact, h[m][q]);
+                        for (int q = 0; q < 4; ++q) v[q] = v[q] * trn::act_grad(a.dact, h[m][q]);
+                    }
+                    *reinterpret_cast<f32x4*>(a.out2 + s * a.ld_out + 16 * m + 4 * g) = v;
                 }
-                *reinterpret_cast<f32x4*>(a.out2 + s * a.ld_out + 16 * m + 4 * g) = v;
             }
         }
     }
