@@ -776,7 +776,13 @@ __device__ __forceinline__ void sfor(F&& f) {
     sfor_impl(f, std::make_integer_sequence<int, N>{});
 }
 #if DF_LDW_DMA
-__device__ __forceinline__ int ldw_slot(int row, int sg) { return sg ^ ((-(row >> 2)) & 3); }
+// 16-B slot of 8-sample group sg in plane row `row` (64-B rows): sg XOR bits 1..2 of the row.
+// Conflict-free for the MFMA phase's fragment ds_read_b128 (banks (a/4) mod 64, lane groups
+// {0–3,12–15,20–27}, ... : 16 distinct (row mod 4, slot) pairs each) and for ds_write_b128 of
+// 8 consecutive rows (banks (a/4) mod 32, 8 contiguous lanes: 8 distinct (row mod 2, slot)
+// pairs) — MI355X_MICROARCH.md §LDS.  (The round-3 slot sg XOR (−(row >> 2)) & 3 made every
+// plane store 2-way: 192 conflict cycles per wave and step, profiles/r05_ldw_lds_conflicts.txt.)
+__device__ __forceinline__ int ldw_slot(int row, int sg) { return sg ^ ((row >> 1) & 3); }
 
 // H0R (training with feature snapshots, LdwArgs::feat): the second operand, H0, is not
 // read from HBM but recomputed per step from the net's 32-float feature rows with the wide
@@ -898,17 +904,23 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
                 });
                 uni::bf16x8 p[3];
                 split8x(f32x4{hv[0], hv[1], hv[2], hv[3]}, f32x4{hv[4], hv[5], hv[6], hv[7]}, p[0], p[1], p[2]);
+                // lane groups g, g ^ 1 hold the two halves (samples 8sg .. +3, +4 .. +7) of
+                // the 16-B slots of rows R + j (hh = 0) and R + 16 + j (hh = 1): one
+                // v_permlane16_swap per dword gives even groups the whole hh = 0 slot, odd
+                // groups the hh = 1 slot, stored by one ds_write_b128 (8 consecutive rows per
+                // lane group of the store: conflict-free with ldw_slot)
                 const int sgp = 2 * tt + (g >> 1);  // 8-sample group of samples 16tt + 4g ..
+                const int row = 16 * (4 * wave + 2 * mp2 + (g & 1)) + j;
+                uint8_t* dst = TB + row * 64 + 16 * ldw_slot(row, sgp);
 #pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const int row = 16 * (4 * wave + 2 * mp2 + hh) + j;
-                    uint8_t* dst = TB + row * 64 + 16 * ldw_slot(row, sgp) + 8 * (g & 1);
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        uint64_t u[2];
-                        __builtin_memcpy(u, &p[k], 16);
-                        *reinterpret_cast<uint64_t*>(dst + k * PB) = u[hh];
-                    }
+                for (int k = 0; k < 3; ++k) {
+                    uint32_t u[4];
+                    __builtin_memcpy(u, &p[k], 16);  // dwords 0, 1: hh = 0; 2, 3: hh = 1
+                    const auto s0w = __builtin_amdgcn_permlane16_swap(u[0], u[2], false, false);
+                    const auto s1w = __builtin_amdgcn_permlane16_swap(u[1], u[3], false, false);
+                    // even g: (own hh = 0, g + 1's hh = 0); odd g: (g − 1's hh = 1, own hh = 1)
+                    const uint32_t o[4] = {s0w[0], s1w[0], s0w[1], s1w[1]};
+                    *reinterpret_cast<uint4*>(dst + k * PB) = uint4{o[0], o[1], o[2], o[3]};
                 }
             });
         });
@@ -916,11 +928,9 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
         // workgroup is a multiple of 32): mask block (s0 / 32, wave), one dword a lane
         a.hmask[((s0 >> 5) * 4 + wave) * 64 + lane] = mv;
     };
-    // step 2 for one operand: rows 4q + i, samples 8sg + e
-    // Rows q + 64i (not 4q + i): the 16 lanes of a plane write then cover all 16
-    // (row & 3, slot) pairs, i.e. all 64 banks (rows 4 apart sit 256 B apart: one bank
-    // group per slot, 16-way).  The stage reads become dword reads of 64 consecutive
-    // floats (conflict-free).  swz: the H0R rows (quad XOR (s & 15)).
+    // step 2 for one operand: rows q + 64i, samples 8sg + e (the 8 contiguous lanes of a
+    // plane store: 8 consecutive rows; the stage reads: dword reads of 64 consecutive floats,
+    // conflict-free).  swz: rows stored with the quad XOR (s & 15) swizzle (unused).
     auto split_item = [&](int op, uint8_t* T, bool db, bool swz) {
         float x[4][8];
 #pragma unroll
