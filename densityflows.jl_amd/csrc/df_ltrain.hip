@@ -20,9 +20,13 @@ using impl::mfma4;
 #ifndef DF_LT_MREM
 #define DF_LT_MREM 0
 #endif
+#ifndef DF_LDW_MREM  // the split dW kernel's own choice (its matrix pipe idles in the split phase)
+#define DF_LDW_MREM DF_LT_MREM
+#endif
+template <bool MREM = (DF_LT_MREM != 0)>
 __device__ __forceinline__ void split8x(const f32x4& a, const f32x4& b, uni::bf16x8& p0, uni::bf16x8& p1,
                                         uni::bf16x8& p2) {
-    if constexpr (DF_LT_MREM) {
+    if constexpr (MREM) {
         uni::split8_mrem(uni::neg_eye(), a, b, p0, p1, p2);
     } else {
         const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
@@ -873,7 +877,7 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
     auto h0_compute = [&](int64_t s0, const f32x4 (&fr)[2][2], const W0In& w0) {
         uni::bf16x8 x[2][3];  // A operand: lane (g, i) holds features 8g + e of sample 16tt + i
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) split8x(fr[tt][0], fr[tt][1], x[tt][0], x[tt][1], x[tt][2]);
+        for (int tt = 0; tt < 2; ++tt) split8x<DF_LDW_MREM != 0>(fr[tt][0], fr[tt][1], x[tt][0], x[tt][1], x[tt][2]);
         const bool full = s0 + 32 <= s_end;  // (uniform) no sample of the step past the range
         uint32_t mv = 0u;                    // this lane's dword of the wave's relu-mask block
         // (compile-time loops: the mask's v_writelane takes its lane as an inline constant)
@@ -903,7 +907,7 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
                     for (int r = 0; r < 4; ++r) mv |= (hv[4 * hh + r] > 0.f ? 1u : 0u) << (4 * (2 * mm + tt) + r);
                 });
                 uni::bf16x8 p[3];
-                split8x(f32x4{hv[0], hv[1], hv[2], hv[3]}, f32x4{hv[4], hv[5], hv[6], hv[7]}, p[0], p[1], p[2]);
+                split8x<DF_LDW_MREM != 0>(f32x4{hv[0], hv[1], hv[2], hv[3]}, f32x4{hv[4], hv[5], hv[6], hv[7]}, p[0], p[1], p[2]);
                 // lane groups g, g ^ 1 hold the two halves (samples 8sg .. +3, +4 .. +7) of
                 // the 16-B slots of rows R + j (hh = 0) and R + 16 + j (hh = 1): one
                 // v_permlane16_swap per dword gives even groups the whole hh = 0 slot, odd
@@ -945,7 +949,7 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
         for (int i = 0; i < 4; ++i) {
             const float(&v)[8] = x[i];
             uni::bf16x8 p0, p1, p2;
-            split8x(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, p0, p1, p2);
+            split8x<DF_LDW_MREM != 0>(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, p0, p1, p2);
             const int row = q + 64 * i;
             uint8_t* dst = T + row * 64 + 16 * ldw_slot(row, sg);
             *reinterpret_cast<uni::bf16x8*>(dst) = p0;
