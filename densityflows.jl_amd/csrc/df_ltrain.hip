@@ -845,9 +845,9 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
     // hits: 48 KiB read by every workgroup), their latency under the δ split: held through
     // the MFMA phase they would spill.  The pointers are opaque per step (as loop invariants
     // the loads would be hoisted out of the loop).
-    struct W0In {
-        uni::bf16x8 w[NM][3];
-        float b[NM];
+    struct W0In {  // (sized for H0R: the other instance never declares one)
+        uni::bf16x8 w[4][3];
+        float b[4];
     };
     auto h0_wload = [&](W0In& in) {
         const uint8_t* w0p = a.w0s;

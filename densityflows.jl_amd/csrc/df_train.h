@@ -30,6 +30,16 @@ namespace df {
 #endif
 constexpr int kTrainWaves = DF_TRAIN_WAVES;     // waves per workgroup of the fused net kernel
 constexpr int kTrainThreads = 64 * kTrainWaves;
+// 16-sample tiles one wave of a SPLIT instance carries through the sweep together: with
+// 2, a workgroup is kTrainWaves / 2 waves (one per SIMD, VGPRs + AGPRs = 512 per lane)
+// and each wave interleaves two independent tiles (df_train_impl.h).  The per-SIMD tile
+// count, the LDS transpose area and the tiles per workgroup pass are unchanged.
+#ifndef DF_TRAIN_TT
+#define DF_TRAIN_TT 1
+#endif
+constexpr int kTrainSplitTT = DF_TRAIN_TT;
+static_assert(kTrainWaves % kTrainSplitTT == 0, "tiles per wave must divide the workgroup's tile count");
+constexpr int train_threads(bool split) { return split ? kTrainThreads / kTrainSplitTT : kTrainThreads; }
 // Per-wave transpose buffers [row][16 samples] (df_train_impl.h): rows of 20 floats (row
 // R and R + 4 of a ds_write_b32 half-wave hit disjoint bank halves) and, with
 // DF_TRAIN_SWZ, the 4-float column quads XOR-swizzled by row (trn::rswz: Gray bit of

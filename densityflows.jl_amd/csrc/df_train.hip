@@ -168,13 +168,13 @@ hipError_t launch_train_net(int ht, int nh, int am, const TrainArgs& a, unsigned
     void* k = train_ptr(ht, nh, am, a.net.split != 0, naf);
     if (!k) return hipErrorInvalidValue;
     void* args[] = {const_cast<TrainArgs*>(&a)};
-    return hipLaunchKernel(k, dim3(grid), dim3(kTrainThreads), args, lds, st);
+    return hipLaunchKernel(k, dim3(grid), dim3(train_threads(a.net.split != 0)), args, lds, st);
 }
 
 hipError_t train_net_occupancy(int ht, int nh, int am, size_t lds, int* blocks, bool split) {
     void* k = train_ptr(ht, nh, am, split);
     if (!k) return hipErrorInvalidValue;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k, kTrainThreads, lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k, train_threads(split), lds);
 }
 
 hipError_t launch_scale(float* dst, const float* src, float s, int64_t count, hipStream_t st) {

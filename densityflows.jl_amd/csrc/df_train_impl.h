@@ -1,6 +1,8 @@
 // df_train_impl.h — the reverse-sweep kernel of one conditioner net.
 //
-// Every wave owns 16-sample tiles (persistent grid).  Per tile:
+// Every wave owns 16-sample tiles (persistent grid); a SPLIT instance's wave carries
+// kTrainSplitTT of them through every step together (df_train.h: one wave per SIMD,
+// two independent chains per wave).  Per tile:
 //   forward recompute   x → A0 = σ0(W0 x + b0) [→ A1 = σh(W1 A0 + b1)] → y = σo(W3 h + b3)
 //                       (same device functions and rounding as the inverse
 //                       pass, so s and t are bitwise those of step 1);
@@ -143,6 +145,32 @@ __device__ __forceinline__ uni::bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// The three planes of 4 values as one run [p1 p0 p2] (DF_TRAIN_DW1_CONTIG): both SPLIT
+// dW1 operands of a row tile are 4-dword windows of it.
+#ifndef DF_TRAIN_DW1_CONTIG
+#define DF_TRAIN_DW1_CONTIG 1
+#endif
+typedef __bf16 bf16x12 __attribute__((ext_vector_type(12)));
+
+__device__ __forceinline__ bf16x12 split4_run(f32x4 v) {
+    bf16x12 q;
+#pragma unroll
+    for (int e = 0; e < 4; e += 2) {
+        uni::bf16x2 h, m, l;
+        uni::split2(v[e], v[e + 1], h, m, l);
+        q[e] = m[0]; q[e + 1] = m[1];
+        q[4 + e] = h[0]; q[5 + e] = h[1];
+        q[8 + e] = l[0]; q[9 + e] = l[1];
+    }
+    return q;
+}
+__device__ __forceinline__ uni::bf16x8 run_lo(const bf16x12& q) {  // [p1 | p0]
+    return __builtin_shufflevector(q, q, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ uni::bf16x8 run_hi(const bf16x12& q) {  // [p0 | p2]
+    return __builtin_shufflevector(q, q, 4, 5, 6, 7, 8, 9, 10, 11);
+}
+
 // dW_out and dW0 of the SPLIT instances (one first-Dense k-step: <= 4 features, <= 4
 // outputs) on v_mfma_f32_4x4x1_16b_f32: 16 blocks of 4×4, one sample per instruction,
 // block b = lane / 4 owning hidden rows 4b..4b+3 — no zero-padded rows (the 16x16x4
@@ -159,12 +187,16 @@ __device__ __forceinline__ f32x4 mfma4x4(float a, float b, f32x4 c) {
 // 2 and 3: the d = 5 chains; the launcher also requires ≤ 4 conditioner inputs);
 // 0: a.n_af at run time.
 template <int HT, int NH, int AM, bool SPLIT = false, int NAF = 0>
-__global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a) {
+__global__ void __launch_bounds__(train_threads(SPLIT), 1) train_net_kernel(TrainArgs a) {
     using namespace trn;
     const int n_af = NAF > 0 ? NAF : a.n_af;
     constexpr bool RELU = (AM == AM_RELU);
     constexpr bool PRE = (AM == AM_PRE);
     constexpr bool M4 = SPLIT && DF_TRAIN_M4;
+    // tiles per wave (df_train.h kTrainSplitTT): every per-tile step below runs over the TT
+    // tiles back to back, so one wave issues two independent chains
+    constexpr int TT = SPLIT ? kTrainSplitTT : 1;
+    constexpr int NW = kTrainWaves / TT, NT = 64 * NW;  // waves, threads per workgroup
     static_assert(!SPLIT || (RELU && NH == 1 && HT >= 2), "SPLIT: relu nets with one hidden Dense, hidden 32/64");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const GNet& G = a.net;
@@ -181,34 +213,38 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
     const int d = a.d, n = a.n;
     constexpr int TROWS = 16 * HT;
     constexpr int INP = 16 * HT;
-    float* TA = tarea + wave * 2 * TROWS * kTS;
-    float* TB = TA + TROWS * kTS;
+    // transpose buffers of tile t of this wave: TA(t) (δ side), TB(t) (activation side)
+    float* const TW = tarea + wave * TT * 2 * TROWS * kTS;
+    auto TA = [&](int t) { return TW + t * 2 * TROWS * kTS; };
+    auto TB = [&](int t) { return TW + t * 2 * TROWS * kTS + TROWS * kTS; };
     const bool sph = (a.phase == TR_PHASE_S);
     const bool rnvp = (a.kind == DF_LAYER_RNVP);
 
     {  // the net's forward and transposed fragments → LDS
         const f32x4* src = reinterpret_cast<const f32x4*>(SPLIT ? a.sblob + G.sfwd_src : a.blob + G.fwd_src);
-        for (int i = tid; i < fwd_bytes / 16; i += kTrainThreads) reinterpret_cast<f32x4*>(fw)[i] = src[i];
+        for (int i = tid; i < fwd_bytes / 16; i += NT) reinterpret_cast<f32x4*>(fw)[i] = src[i];
         const f32x4* srt = reinterpret_cast<const f32x4*>(a.tblob + G.t_src);
         if constexpr (NAF > 0) {
             // W0ᵀ alone (SPLIT), read only by the 4x4x1 x̄, which takes the fragments of lanes
             // (lane & 3) + 16g: those 16 per k-quad go to slots (lane & 3) + 4g, one 256-byte
             // run (its ds_read_b128 then hit 16 distinct bank groups instead of 4)
             const int w0 = G.off_w0t / 16;
-            for (int i = tid; i < HT * 16; i += kTrainThreads) {
+            for (int i = tid; i < HT * 16; i += NT) {
                 const int kq = i >> 4, c = i & 15;
                 reinterpret_cast<f32x4*>(tw)[w0 + kq * 64 + c] = srt[w0 + kq * 64 + (c & 3) + 16 * (c >> 2)];
             }
         } else {
-            for (int i = tid; i < t_bytes / 16; i += kTrainThreads) reinterpret_cast<f32x4*>(tw)[i] = srt[i];
+            for (int i = tid; i < t_bytes / 16; i += NT) reinterpret_cast<f32x4*>(tw)[i] = srt[i];
         }
         if constexpr (SPLIT) {
             const f32x4* sst = reinterpret_cast<const f32x4*>(a.tsblob + G.st_src);
-            for (int i = tid; i < G.st_bytes / 16; i += kTrainThreads) reinterpret_cast<f32x4*>(stw)[i] = sst[i];
+            for (int i = tid; i < G.st_bytes / 16; i += NT) reinterpret_cast<f32x4*>(stw)[i] = sst[i];
         }
     }
-    // zero rows of the δ_out transpose that no lane writes (rows >= 4)
-    for (int i = lane; i < TROWS * kTS; i += 64) TA[i] = 0.f;
+    // zero rows of the δ_out transposes that no lane writes (rows >= 4)
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+        for (int i = lane; i < TROWS * kTS; i += 64) TA(t)[i] = 0.f;
     __syncthreads();
 
     constexpr int NHT = NH ? HT : 1;
@@ -287,11 +323,17 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
         for (int r = 0; r < 4; ++r) zxv[r] = (ok && zxc(r) != 0xff) ? a.zbar[s * d + zxc(r)] : 0.f;
     };
 
+    // wave-tile-group p holds the TT consecutive tiles TT·p .. TT·p + TT − 1
     const int64_t ntiles = (a.batch + 15) / 16;
-    const int64_t tstride = (int64_t)gridDim.x * kTrainWaves;
-    for (int64_t tile = (int64_t)blockIdx.x * kTrainWaves + wave; tile < ntiles; tile += tstride) {
-        const int64_t s = tile * 16 + j;
-        const bool valid = s < a.batch;
+    const int64_t pstride = (int64_t)gridDim.x * NW;
+    for (int64_t p = (int64_t)blockIdx.x * NW + wave; p * TT < ntiles; p += pstride) {
+        int64_t s[TT];
+        bool valid[TT];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            s[t] = (p * TT + t) * 16 + j;
+            valid[t] = s[t] < a.batch;
+        }
         zxl = zxp8;
         afl = afp8;
         asm volatile("" : "+v"(zxl), "+v"(afl));
@@ -300,59 +342,63 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
             xcl[r] = xcode[r];
             asm volatile("" : "+v"(xcl[r]));
         }
-        float xr[4], zbp[4], aux[4], zxp[4];
-        load_x(s, valid, xr);
+        float xr[TT][4], zbp[TT][4], aux[TT][4], zxp[TT][4];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) load_x(s[t], valid[t], xr[t]);
 
         // ---- conditioner input, features k = 4r + g of vcat(θ, u)[axis_nn] ----
-        float xin[1][4];
+        float xin[TT][4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float v = xr[r];
-            const int kind = xcl[r] >> 8;
-            if (kind == 1 && a.tmin) {  // normalize_input (Data.jl:213-218)
-                const int slot = xcl[r] & 0xff;
-                const float lo = a.tmin[slot], diff = a.tmax[slot] - lo;
-                v = (diff == 0.f) ? 0.f : (v - lo) / diff;
+        for (int t = 0; t < TT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v = xr[t][r];
+                const int kind = xcl[r] >> 8;
+                if (kind == 1 && a.tmin) {  // normalize_input (Data.jl:213-218)
+                    const int slot = xcl[r] & 0xff;
+                    const float lo = a.tmin[slot], diff = a.tmax[slot] - lo;
+                    v = (diff == 0.f) ? 0.f : (v - lo) / diff;
+                }
+                if (kind == 3) v = 1.f;
+                xin[t][r] = valid[t] ? v : 0.f;
             }
-            if (kind == 3) v = 1.f;
-            xin[0][r] = valid ? v : 0.f;
-        }
 
         // ---- forward recompute ----
-        f32x4 A0[1][HT], A1[1][HT];
+        f32x4 A0[TT][HT], A1[TT][HT];
         constexpr int NP = PRE ? HT : 1;
-        f32x4 D0[NP], D1[NP];  // AM_PRE: σ'(pre) of the first / hidden Dense
+        f32x4 D0[NP], D1[NP];  // AM_PRE (TT = 1): σ'(pre) of the first / hidden Dense
         if constexpr (SPLIT) {  // the inverse pass's SPLIT kernel functions: bitwise its s and t
-            uni::dense_first_split<HT, 1>(fw, N, xin, A0);
-            uni::bias_act<HT, 1, true>(fw, DF_ACT_RELU, A0, false);
+            uni::dense_first_split<HT, TT>(fw, N, xin, A0);
+            uni::bias_act<HT, TT, true>(fw, DF_ACT_RELU, A0, false);
         } else {
-            uni::dense_first<HT, 1>(fw, N, xin, A0);
+            uni::dense_first<HT, TT>(fw, N, xin, A0);
         }
         if constexpr (SPLIT) {
         } else if constexpr (PRE) {
-            uni::bias_act<HT, 1, false>(fw + N.off_b0, DF_ACT_IDENTITY, A0, !N.fold0);
+            uni::bias_act<HT, TT, false>(fw + N.off_b0, DF_ACT_IDENTITY, A0, !N.fold0);
             act_keep_grad<HT>(N.act0, A0[0], D0);
         } else {
-            uni::bias_act<HT, 1, RELU>(fw + N.off_b0, N.act0, A0, !N.fold0);
+            uni::bias_act<HT, TT, RELU>(fw + N.off_b0, N.act0, A0, !N.fold0);
         }
-        load_pull(s, valid, zbp, aux);
+#pragma unroll
+        for (int t = 0; t < TT; ++t) load_pull(s[t], valid[t], zbp[t], aux[t]);
         if constexpr (SPLIT) {
-            uni::dense_hidden_split<HT, 1, true, true>(fw + N.off_h, A0, A1);
-            uni::bias_act<HT, 1, true>(fw, DF_ACT_RELU, A1, false);
+            uni::dense_hidden_split<HT, TT, true, true>(fw + N.off_h, A0, A1);
+            uni::bias_act<HT, TT, true>(fw, DF_ACT_RELU, A1, false);
         } else if constexpr (NH == 1) {
-            uni::dense_hidden<HT, 1>(fw + N.off_h, A0, A1);
+            uni::dense_hidden<HT, TT>(fw + N.off_h, A0, A1);
             if constexpr (PRE) {
-                uni::bias_act<HT, 1, false>(fw + N.off_h + HT * HT * 1024, DF_ACT_IDENTITY, A1);
+                uni::bias_act<HT, TT, false>(fw + N.off_h + HT * HT * 1024, DF_ACT_IDENTITY, A1);
                 act_keep_grad<HT>(N.acth, A1[0], D1);
             } else {
-                uni::bias_act<HT, 1, RELU>(fw + N.off_h + HT * HT * 1024, N.acth, A1);
+                uni::bias_act<HT, TT, RELU>(fw + N.off_h + HT * HT * 1024, N.acth, A1);
             }
         }
-        const f32x4(&H)[1][HT] = NH ? A1 : A0;
-        f32x4 o[1];
+        const f32x4(&H)[TT][HT] = NH ? A1 : A0;
+        f32x4 o[TT];
         float dfo[4] = {1.f, 1.f, 1.f, 1.f};  // AM_PRE: σo'(pre) of the output Dense
         if constexpr (PRE) {
-            uni::out_valu<HT, 1, true, NAF>(fw, N, H, o);  // pre-activation (no σo)
+            uni::out_valu<HT, TT, true, NAF>(fw, N, H, o);  // pre-activation (no σo)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float x = o[0][k];
@@ -361,174 +407,230 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
                 o[0][k] = y;
             }
         } else {
-            uni::out_valu<HT, 1, RELU, NAF>(fw, N, H, o);
+            uni::out_valu<HT, TT, RELU, NAF>(fw, N, H, o);
         }
 
         // ---- coupling pullback → ȳ (every lane group holds all outputs of sample j) ----
-        float dout[4], zb[4], ee[4];
+        float dout[TT][4], zb[TT][4], ee[TT][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            dout[k] = 0.f;
-            zb[k] = 0.f;
-            ee[k] = 1.f;
-            if (k < n_af && valid) {
-                zb[k] = zbp[k];
-                if (sph) {
-                    ee[k] = expf(-o[0][k]);
-                    dout[k] = -zb[k] * aux[k] + a.inv_n;  // s̄ = -z̄_af·z_af - j̄
-                } else {
-                    if (rnvp) ee[k] = aux[k];
-                    dout[k] = -zb[k] * ee[k];             // t̄ = -z̄_af·exp(-s)
-                }
-                if (PRE) {
-                    if (N.act_out != DF_ACT_IDENTITY) dout[k] = dout[k] * dfo[k];
-                } else if (!RELU && N.act_out != DF_ACT_IDENTITY) {
-                    dout[k] = dout[k] * act_grad(N.act_out, o[0][k]);
-                }
-            }
-        }
-        if (sph && g == 0 && valid) {
+        for (int t = 0; t < TT; ++t)
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (k < n_af) a.ebuf[s * 4 + k] = ee[k];
-        }
-
-        // ---- output Dense: dW3 += ȳ·hᵀ, db3 += Σȳ, h̄ = W3ᵀ ȳ ----
-        if (g == 0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) TA[tidx(r, j)] = dout[r];
-        }
-        t_write<HT>(TB, H[0]);
-        lds_order();
-        if constexpr (M4) {  // block b: A = ȳ[lane % 4][s], B = h[lane][s], one sample s per step
-            const f32x4 fa = tread(TA, j, g);
-            gbo += hsum4(fa);
-            f32x4 yv[4], hv[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                yv[q] = tread(TA, lane & 3, q);
-                hv[q] = tread(TB, lrow, q);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) gWo4 = mfma4x4(yv[q][e], hv[q][e], gWo4);
-        } else {
-            const f32x4 fa = tread(TA, j, g);
-            gbo += hsum4(fa);
-#pragma unroll
-            for (int mb = 0; mb < HT; ++mb) {
-                const f32x4 fb = tread(TB, 16 * mb + j, g);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) gWo[mb] = mfma4(fa[q], fb[q], gWo[mb]);
-            }
-        }
-        f32x4 hb[1][HT];
-#pragma unroll
-        for (int m = 0; m < HT; ++m) hb[0][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < n_af) {
-#pragma unroll
-                for (int m = 0; m < HT; ++m) {
-                    const f32x4 w = impl::lds4(fw + N.off_out + ((k * INP + 16 * m + 4 * g) << 2));
-                    hb[0][m] = hb[0][m] + w * dout[k];
-                }
-            }
-        }
-        if constexpr (PRE) {
-            const f32x4(&DH)[NP] = NH ? D1 : D0;
-#pragma unroll
-            for (int m = 0; m < HT; ++m) hb[0][m] = hb[0][m] * DH[m];
-        } else {
-            mul_act_grad<HT, RELU>(NH ? N.acth : N.act0, H[0], hb[0]);
-        }
-
-        // ---- hidden Dense: dW1 += δ·A0ᵀ, db1 += Σδ, Ā0 = W1ᵀ δ ----
-        f32x4 d0[1][HT];
-        if constexpr (NH == 1) {
-            lds_order();
-            t_write<HT>(TA, hb[0]);
-            t_write<HT>(TB, A0[0]);
-            lds_order();
-            f32x4 fa[HT], fb[HT];
-#pragma unroll
-            for (int m = 0; m < HT; ++m) {
-                fa[m] = tread(TA, 16 * m + j, g);
-                fb[m] = tread(TB, 16 * m + j, g);
-                gbh[m] += hsum4(fa[m]);
-            }
-            if constexpr (SPLIT) {
-                // k-slot (g, e) of MFMA u: sample 4g + (e & 3), product 2u + (e >> 2) of
-                // (w0x0, w0x1 | w1x0, w0x2 | w1x1, w2x0), δ rows as A, A0 rows as B
-                bf16x4 pb[HT][3];
-#pragma unroll
-                for (int m = 0; m < HT; ++m) split4(fb[m], pb[m][0], pb[m][1], pb[m][2]);
-#pragma unroll
-                for (int ma = 0; ma < HT; ++ma) {
-                    bf16x4 pa[3];
-                    split4(fa[ma], pa[0], pa[1], pa[2]);
-                    const uni::bf16x8 a0 = cat8(pa[1], pa[2]), a1 = cat8(pa[1], pa[0]), a2 = cat8(pa[0], pa[0]);
-#pragma unroll
-                    for (int mb = 0; mb < HT; ++mb) {  // small terms first
-                        f32x4 v = gWh[ma][mb];
-                        v = uni::mfma_bf(a0, cat8(pb[mb][1], pb[mb][0]), v);
-                        v = uni::mfma_bf(a1, cat8(pb[mb][0], pb[mb][2]), v);
-                        gWh[ma][mb] = uni::mfma_bf(a2, cat8(pb[mb][0], pb[mb][1]), v);
+            for (int k = 0; k < 4; ++k) {
+                dout[t][k] = 0.f;
+                zb[t][k] = 0.f;
+                ee[t][k] = 1.f;
+                if (k < n_af && valid[t]) {
+                    zb[t][k] = zbp[t][k];
+                    if (sph) {
+                        ee[t][k] = expf(-o[t][k]);
+                        dout[t][k] = -zb[t][k] * aux[t][k] + a.inv_n;  // s̄ = -z̄_af·z_af - j̄
+                    } else {
+                        if (rnvp) ee[t][k] = aux[t][k];
+                        dout[t][k] = -zb[t][k] * ee[t][k];             // t̄ = -z̄_af·exp(-s)
+                    }
+                    if (PRE) {
+                        if (N.act_out != DF_ACT_IDENTITY) dout[t][k] = dout[t][k] * dfo[k];
+                    } else if (!RELU && N.act_out != DF_ACT_IDENTITY) {
+                        dout[t][k] = dout[t][k] * act_grad(N.act_out, o[t][k]);
                     }
                 }
-            } else {
+            }
+#pragma unroll
+        for (int t = 0; t < TT; ++t)
+            if (sph && g == 0 && valid[t]) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < n_af) a.ebuf[s[t] * 4 + k] = ee[t][k];
+            }
+
+        // ---- output Dense: dW3 += ȳ·hᵀ, db3 += Σȳ, h̄ = W3ᵀ ȳ ----
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            if (g == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) TA(t)[tidx(r, j)] = dout[t][r];
+            }
+            t_write<HT>(TB(t), H[t]);
+        }
+        lds_order();
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+            if constexpr (M4) {  // block b: A = ȳ[lane % 4][s], B = h[lane][s], one sample s per step
+                const f32x4 fa = tread(TA(t), j, g);
+                gbo += hsum4(fa);
+                f32x4 yv[4], hv[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    yv[q] = tread(TA(t), lane & 3, q);
+                    hv[q] = tread(TB(t), lrow, q);
+                }
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
 #pragma unroll
-                    for (int ma = 0; ma < HT; ++ma)
-#pragma unroll
-                        for (int mb = 0; mb < HT; ++mb) gWh[ma][mb] = mfma4(fa[ma][q], fb[mb][q], gWh[ma][mb]);
-            }
-            load_zx(s, valid, zxp);
-            if constexpr (SPLIT) uni::dense_hidden_split<HT, 1, false, true>(stw, hb, d0);
-            else uni::dense_hidden<HT, 1>(tw + G.off_ht, hb, d0);
-            if constexpr (PRE) {
-#pragma unroll
-                for (int m = 0; m < HT; ++m) d0[0][m] = d0[0][m] * D0[m];
+                    for (int e = 0; e < 4; ++e) gWo4 = mfma4x4(yv[q][e], hv[q][e], gWo4);
             } else {
-                mul_act_grad<HT, RELU>(N.act0, A0[0], d0[0]);
+                const f32x4 fa = tread(TA(t), j, g);
+                gbo += hsum4(fa);
+#pragma unroll
+                for (int mb = 0; mb < HT; ++mb) {
+                    const f32x4 fb = tread(TB(t), 16 * mb + j, g);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) gWo[mb] = mfma4(fa[q], fb[q], gWo[mb]);
+                }
+            }
+        }
+        f32x4 hb[TT][HT];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+#pragma unroll
+            for (int m = 0; m < HT; ++m) hb[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k < n_af) {
+#pragma unroll
+                    for (int m = 0; m < HT; ++m) {
+                        const f32x4 w = impl::lds4(fw + N.off_out + ((k * INP + 16 * m + 4 * g) << 2));
+                        hb[t][m] = hb[t][m] + w * dout[t][k];
+                    }
+                }
+            }
+            if constexpr (PRE) {
+                const f32x4(&DH)[NP] = NH ? D1 : D0;
+#pragma unroll
+                for (int m = 0; m < HT; ++m) hb[t][m] = hb[t][m] * DH[m];
+            } else {
+                mul_act_grad<HT, RELU>(NH ? N.acth : N.act0, H[t], hb[t]);
+            }
+        }
+
+        // ---- hidden Dense: dW1 += δ·A0ᵀ, db1 += Σδ, Ā0 = W1ᵀ δ ----
+        f32x4 d0[TT][HT];
+        if constexpr (NH == 1) {
+            lds_order();
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                t_write<HT>(TA(t), hb[t]);
+                t_write<HT>(TB(t), A0[t]);
+            }
+            lds_order();
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                f32x4 fa[HT], fb[HT];
+#pragma unroll
+                for (int m = 0; m < HT; ++m) {
+                    fa[m] = tread(TA(t), 16 * m + j, g);
+                    fb[m] = tread(TB(t), 16 * m + j, g);
+                    gbh[m] += hsum4(fa[m]);
+                }
+                if constexpr (SPLIT && DF_TRAIN_DW1_CONTIG) {
+                    // Planes of 4 samples in one 6-dword run per row tile, [p1 p0 p2]: its
+                    // dwords 0-3 ([p1|p0]) and 2-5 ([p0|p2]) are the MFMA operands, no
+                    // operand assembly.  k-slot (g, e): sample 4g + (e & 3), plane pair
+                    // e >> 2; small terms first:  δ[p0|p2]·A0[p1|p0] = δ0·a1 + δ2·a0,
+                    // δ[p1|p0]·A0[p0|p2] = δ1·a0 + δ0·a2,  δ[p1|p0]·A0[p1|p0] = δ1·a1 + δ0·a0.
+                    bf16x12 qb[HT];
+#pragma unroll
+                    for (int m = 0; m < HT; ++m) qb[m] = split4_run(fb[m]);
+#pragma unroll
+                    for (int ma = 0; ma < HT; ++ma) {
+                        const bf16x12 qa = split4_run(fa[ma]);
+                        const uni::bf16x8 a_lo = run_lo(qa), a_hi = run_hi(qa);
+#pragma unroll
+                        for (int mb = 0; mb < HT; ++mb) {
+                            const uni::bf16x8 b_lo = run_lo(qb[mb]), b_hi = run_hi(qb[mb]);
+                            f32x4 v = gWh[ma][mb];
+                            v = uni::mfma_bf(a_hi, b_lo, v);
+                            v = uni::mfma_bf(a_lo, b_hi, v);
+                            gWh[ma][mb] = uni::mfma_bf(a_lo, b_lo, v);
+                        }
+                    }
+                } else if constexpr (SPLIT) {
+                    // k-slot (g, e) of MFMA u: sample 4g + (e & 3), product 2u + (e >> 2) of
+                    // (w0x0, w0x1 | w1x0, w0x2 | w1x1, w2x0), δ rows as A, A0 rows as B
+                    bf16x4 pb[HT][3];
+#pragma unroll
+                    for (int m = 0; m < HT; ++m) split4(fb[m], pb[m][0], pb[m][1], pb[m][2]);
+#pragma unroll
+                    for (int ma = 0; ma < HT; ++ma) {
+                        bf16x4 pa[3];
+                        split4(fa[ma], pa[0], pa[1], pa[2]);
+                        const uni::bf16x8 a0 = cat8(pa[1], pa[2]), a1 = cat8(pa[1], pa[0]), a2 = cat8(pa[0], pa[0]);
+#pragma unroll
+                        for (int mb = 0; mb < HT; ++mb) {  // small terms first
+                            f32x4 v = gWh[ma][mb];
+                            v = uni::mfma_bf(a0, cat8(pb[mb][1], pb[mb][0]), v);
+                            v = uni::mfma_bf(a1, cat8(pb[mb][0], pb[mb][2]), v);
+                            gWh[ma][mb] = uni::mfma_bf(a2, cat8(pb[mb][0], pb[mb][1]), v);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+#pragma unroll
+                        for (int ma = 0; ma < HT; ++ma)
+#pragma unroll
+                            for (int mb = 0; mb < HT; ++mb) gWh[ma][mb] = mfma4(fa[ma][q], fb[mb][q], gWh[ma][mb]);
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < TT; ++t) load_zx(s[t], valid[t], zxp[t]);
+            if constexpr (SPLIT) uni::dense_hidden_split<HT, TT, false, true>(stw, hb, d0);
+            else uni::dense_hidden<HT, TT>(tw + G.off_ht, hb, d0);
+#pragma unroll
+            for (int t = 0; t < TT; ++t) {
+                if constexpr (PRE) {
+#pragma unroll
+                    for (int m = 0; m < HT; ++m) d0[t][m] = d0[t][m] * D0[m];
+                } else {
+                    mul_act_grad<HT, RELU>(N.act0, A0[t], d0[t]);
+                }
             }
         } else {
-            load_zx(s, valid, zxp);
 #pragma unroll
-            for (int m = 0; m < HT; ++m) d0[0][m] = hb[0][m];
+            for (int t = 0; t < TT; ++t) {
+                load_zx(s[t], valid[t], zxp[t]);
+#pragma unroll
+                for (int m = 0; m < HT; ++m) d0[t][m] = hb[t][m];
+            }
         }
 
         // ---- first Dense: dW0 += δ0·xᵀ, db0 += Σδ0, x̄ = W0ᵀ δ0 ----
         lds_order();
-        t_write<HT>(TA, d0[0]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) TB[tidx(4 * r + g, j)] = xin[0][r];
+        for (int t = 0; t < TT; ++t) {
+            t_write<HT>(TA(t), d0[t]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) TB(t)[tidx(4 * r + g, j)] = xin[t][r];
+        }
         lds_order();
-        if constexpr (M4) {  // block b: A = δ0[lane][s], B = x[lane % 4][s]
-            f32x4 dv[4], xv[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                dv[q] = tread(TA, lrow, q);
-                xv[q] = tread(TB, lane & 3, q);
-            }
-            gb0l += (hsum4(dv[0]) + hsum4(dv[1])) + (hsum4(dv[2]) + hsum4(dv[3]));
+        for (int t = 0; t < TT; ++t) {
+            if constexpr (M4) {  // block b: A = δ0[lane][s], B = x[lane % 4][s]
+                f32x4 dv[4], xv[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+                for (int q = 0; q < 4; ++q) {
+                    dv[q] = tread(TA(t), lrow, q);
+                    xv[q] = tread(TB(t), lane & 3, q);
+                }
+                gb0l += (hsum4(dv[0]) + hsum4(dv[1])) + (hsum4(dv[2]) + hsum4(dv[3]));
 #pragma unroll
-                for (int e = 0; e < 4; ++e) gW04 = mfma4x4(dv[q][e], xv[q][e], gW04);
-        } else {
-            const f32x4 fb = tread(TB, j, g);
+                for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int m = 0; m < HT; ++m) {
-                const f32x4 fa = tread(TA, 16 * m + j, g);
-                gb0[m] += hsum4(fa);
+                    for (int e = 0; e < 4; ++e) gW04 = mfma4x4(dv[q][e], xv[q][e], gW04);
+            } else {
+                const f32x4 fb = tread(TB(t), j, g);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) gW0[m] = mfma4(fa[q], fb[q], gW0[m]);
+                for (int m = 0; m < HT; ++m) {
+                    const f32x4 fa = tread(TA(t), 16 * m + j, g);
+                    gb0[m] += hsum4(fa);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) gW0[m] = mfma4(fa[q], fb[q], gW0[m]);
+                }
             }
         }
-        f32x4 xb = f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 xb[TT];
+#pragma unroll
+        for (int t = 0; t < TT; ++t) xb[t] = f32x4{0.f, 0.f, 0.f, 0.f};
         if constexpr (NAF > 0) {
             // ≤ 4 features (the launcher's condition for these instances): x̄ on
             // v_mfma_f32_4x4x1_16b_f32 instead of a 16-row product with ≤ 4 live rows.
@@ -541,27 +643,36 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
             for (int kq = 0; kq < HT; ++kq) {
                 const f32x4 w = impl::lds4(tw + G.off_w0t + kq * 1024 + ((lane & 3) + 4 * g) * 16);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) xb = mfma4x4(w[r], d0[0][kq][r], xb);
+                for (int t = 0; t < TT; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xb[t] = mfma4x4(w[r], d0[t][kq][r], xb[t]);
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) xb[r] = uni::xgroup_sum(xb[r]);
+            for (int t = 0; t < TT; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xb[t][r] = uni::xgroup_sum(xb[t][r]);
         } else {
 #pragma unroll
             for (int kq = 0; kq < HT; ++kq) {
                 const f32x4 w = impl::lds4(tw + G.off_w0t + kq * 1024 + lane * 16);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) xb = mfma4(w[r], d0[0][kq][r], xb);
+                for (int t = 0; t < TT; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xb[t] = mfma4(w[r], d0[t][kq][r], xb[t]);
             }
         }
-        if (valid) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (zxc(r) != 0xff) a.zbar[s * d + zxc(r)] = zxp[r] + xb[r];
-        }
-        if (!sph && rnvp && g == 0 && valid) {  // ū_af = z̄_af·exp(-s)
+        for (int t = 0; t < TT; ++t) {
+            if (valid[t]) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (afc(k) != 0xff) a.zbar[s * d + afc(k)] = zb[k] * ee[k];
+                for (int r = 0; r < 4; ++r)
+                    if (zxc(r) != 0xff) a.zbar[s[t] * d + zxc(r)] = zxp[t][r] + xb[t][r];
+            }
+            if (!sph && rnvp && g == 0 && valid[t]) {  // ū_af = z̄_af·exp(-s)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (afc(k) != 0xff) a.zbar[s[t] * d + afc(k)] = zb[t][k] * ee[t][k];
+            }
         }
         lds_order();
     }
@@ -580,7 +691,7 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
     float* R1 = R0 + ((hp * G.n_in + 3) & ~3);
     float* R2 = R1 + ((NH == 1 ? G.h_true * P1 : 0) + 3 & ~3);
     const int rn = (int)(R2 - R) + sp * G.h_true;
-    for (int i = tid; i < rn; i += kTrainThreads) R[i] = 0.f;
+    for (int i = tid; i < rn; i += NT) R[i] = 0.f;
 #pragma unroll
     for (int m = 0; m < HT; ++m) gb0[m] = uni::xgroup_sum(gb0[m]);
 #pragma unroll
@@ -591,7 +702,7 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
     const int wo0 = G.w_off[0] - G.p_begin, bo0 = G.b_off[0] - G.p_begin;
     const int wo1 = G.w_off[1] - G.p_begin, bo1 = G.b_off[1] - G.p_begin;
     const int wo2 = G.w_off[2] - G.p_begin, bo2 = G.b_off[2] - G.p_begin;
-    for (int w = 0; w < kTrainWaves; ++w) {
+    for (int w = 0; w < NW; ++w) {
         if (wave == w) {
             if constexpr (M4) {
 #pragma unroll
@@ -639,7 +750,7 @@ __global__ void __launch_bounds__(kTrainThreads, 1) train_net_kernel(TrainArgs a
         __syncthreads();
     }
     float* dst = a.partial + (int64_t)blockIdx.x * a.p_total + G.p_begin;
-    for (int i = tid; i < G.p_count; i += kTrainThreads) {
+    for (int i = tid; i < G.p_count; i += NT) {
         const int k0 = i - wo0, k1 = i - wo1, k2 = i - wo2;
         float v = R[i];
         if (k0 >= 0 && k0 < h * G.n_in) {
