@@ -38,8 +38,8 @@ PMC = [
       ("uniform_kernel<4, 3", "uniform_kernel<4, 3, true, true, true, true>")]),
     ("pmct_cfg4", "config-5 train step (bench --mode train --config cfg4)",
      [("sweep_kernel<16, 1>", "sweep_kernel<16, 1>"), ("wide_kernel<3, true>", "wide_kernel<3, true>"),
-      ("ldense_kernel<16, 0, 4, true,", "ldense_kernel<16, 0, 4, true, 8, 2>"),
-      ("ldw_split_kernel", "ldw_split_kernel")]),
+      ("ldense_kernel<16, 0, 5, true,", "ldense_kernel<16, 0, 5, true, 8, 2>"),
+      ("ldw_split_kernel", "ldw_split_kernel<true>")]),
 ]
 OUT = {"pmc_cfg2": "pmc_cfg2", "pmc_cfg4": "pmc_cfg4", "pmct_cfg2": "pmc_train_cfg2", "pmct_cfg4": "pmc_train_cfg5"}
 for d, what, kernels in PMC:
