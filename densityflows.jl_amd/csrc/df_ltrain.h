@@ -95,6 +95,12 @@ struct LDenseArgs {
     const uint8_t* w2frag;
     int nkq2;
     float* out2;            // δ of the last hidden Dense [B][ld_out]
+    // couple_bwd (one output tile, DF_FRONT_DWO): the output Dense's dW = ȳ·Hᵀ and db = Σ ȳ,
+    // accumulated by the front from the H and ȳ it holds and written as the workgroup's
+    // partial row (layout of ldw: w_off + o + m_true·col, b_off + o)
+    float* dwo_partial;
+    int64_t dwo_p_total;
+    int dwo_w_off, dwo_b_off, dwo_m_true, dwo_n_true;
 };
 
 struct LdwArgs {
@@ -142,6 +148,10 @@ hipError_t launch_ldw(const LdwArgs& a, unsigned grid, hipStream_t st);
 // Output Dense + coupling pullback → ȳ, then δ = (W_outᵀ ȳ) ⊙ σ'(H) in one pass over H
 // (ht: 16-row tiles of H, mto: output tiles <= 2).  LDS: both fragment sets.
 hipError_t launch_couple_bwd(int ht, int mto, const LDenseArgs& a, unsigned grid, size_t lds, hipStream_t st);
+// the front computes its net's output-Dense dW / db (mto 1, DF_FRONT_DWO); the extra LDS it
+// needs beyond its fragments, and whether it does
+bool front_dwo(int mto);
+size_t front_dwo_lds(int ht);
 hipError_t set_couple_bwd_lds_limit(size_t lds);
 // conditioner input vcat(θ, u)[axis_nn] → xsave [B][ld_x] (rows >= n_in zero), for dW0
 hipError_t launch_gather_features(const LDenseArgs& a, int rows, hipStream_t st);

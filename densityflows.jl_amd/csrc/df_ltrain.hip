@@ -441,12 +441,40 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
 // the first product and as the σ' argument of the second; ȳ stays in registers as
 // the B operand of the second (accumulator layout = B layout).  One 16-sample tile
 // per wave per round; both fragment sets resident in LDS.
+#ifndef DF_FRONT_DWO
+#define DF_FRONT_DWO 1
+#endif
+// DF_FRONT_DWO (one output tile): the front also accumulates its net's output-Dense dW =
+// ȳ·Hᵀ and db = Σ ȳ from the ȳ and H it already holds — the separate narrow dW product
+// would read H from HBM a second time.  Per tile: ȳ and each 16-row block of H go through
+// a per-wave LDS transpose (trn::t_write / trn::tread: samples onto the MFMA k slots), 4
+// f32 MFMAs per block; the 8 waves are summed in LDS in wave order and each workgroup
+// writes its partial row (bitwise reproducible, like every other dW).
+constexpr int kFrontDwoTS = 16 * kTS;  // floats of one 16-row transpose block
+size_t front_dwo_lds_bytes(int ht) {
+    const size_t tr = (size_t)kWavesPerBlock * 2 * kFrontDwoTS * 4;        // ȳ and H blocks per wave
+    const size_t red = (size_t)16 * (16 * ht + 4) * 4 + (size_t)kWavesPerBlock * 256 * 4;  // dW rows + db lanes
+    return tr > red ? tr : red;
+}
+
 template <int HT, int MTO>
 __device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, int bid, int nb) {
     uint8_t* wo = smem;                         // W_out: [kq < HT][m < MTO]
     uint8_t* wt = smem + HT * MTO * 1024;       // W_outᵀ: [kq < MTO][m < HT]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = lane >> 4, j = lane & 15;
+    constexpr bool DWO = (MTO == 1) && DF_FRONT_DWO;
+#ifndef DF_FRONT_DWO_PF
+#define DF_FRONT_DWO_PF 0
+#endif
+    constexpr bool HPF = !DWO || DF_FRONT_DWO_PF;  // H of the next tile prefetched
+    float* dscr = reinterpret_cast<float*>(smem + 2 * HT * MTO * 1024);  // DWO scratch (front_dwo_lds_bytes)
+    float* Ty = dscr + wave * 2 * kFrontDwoTS;  // this wave's ȳ block [o][sample] ...
+    float* Th = Ty + kFrontDwoTS;               // ... and H block [row][sample]
+    f32x4 gwo[DWO ? HT : 1];                    // dW[o = 4g + r][16kq + j]
+    float gbo[4] = {0.f, 0.f, 0.f, 0.f};        // Σ ȳ[4g + r] over this lane's samples
+#pragma unroll
+    for (int kq = 0; kq < (DWO ? HT : 1); ++kq) gwo[kq] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
         const int n1 = a.nkq * MTO * 64, n2 = a.nkq2 * HT * 64;
         for (int q = tid; q < n1; q += kBlockThreads)
@@ -504,17 +532,19 @@ __device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, 
     // (MTO = 2: the operands of the tile itself, loaded at its pullback — the prefetch's
     // registers would spill there)
     constexpr bool PFP = (MTO == 1);
+    // (DWO: H of the tile loaded at its start — the prefetch's registers hold dW instead)
     if ((int64_t)bid * kWavesPerBlock + wave < ntiles) {
-        load_h((int64_t)bid * kWavesPerBlock + wave);
+        if (HPF) load_h((int64_t)bid * kWavesPerBlock + wave);
         if (PFP) load_p((int64_t)bid * kWavesPerBlock + wave);
     }
     for (int64_t tile = (int64_t)bid * kWavesPerBlock + wave; tile < ntiles; tile += tstride) {
         const int64_t s = tile * 16 + j;
         const bool valid = s < a.batch;
         f32x4 h[HT];
+        if (!HPF) load_h(tile);
 #pragma unroll
         for (int kq = 0; kq < HT; ++kq) h[kq] = hn[kq];
-        if (tile + tstride < ntiles) load_h(tile + tstride);
+        if (HPF && tile + tstride < ntiles) load_h(tile + tstride);
         f32x4 y[MTO];
 #pragma unroll
         for (int m = 0; m < MTO; ++m) y[m] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -599,6 +629,57 @@ __device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, 
                 }
             }
         }
+        if constexpr (DWO) {  // dW += ȳ·Hᵀ over the tile's samples (a padding sample's ȳ is 0)
+            trn::t_write<1>(Ty, dy);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gbo[q] += dy[0][q];
+            const f32x4 ya = trn::tread(Ty, j, g);  // ȳ[o = j][samples 4g .. 4g + 3]
+#pragma unroll
+            for (int kq = 0; kq < HT; ++kq) {
+                if (kq < a.nkq) {
+                    const f32x4 hk[1] = {h[kq]};
+                    trn::t_write<1>(Th, hk);
+                    const f32x4 hb = trn::tread(Th, j, g);  // H[16kq + j][samples 4g ..]
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) gwo[kq] = mfma4(ya[q], hb[q], gwo[kq]);
+                }
+            }
+        }
+    }
+    if constexpr (DWO) {  // workgroup sum in wave order → this workgroup's partial row
+        constexpr int RS = 16 * HT + 4;  // row stride of the dW rows (the two row groups of a b32 half-wave 16 banks apart)
+        float* R = dscr;
+        float* D = dscr + 16 * RS;  // db lanes [wave][64]
+        __syncthreads();
+        for (int w = 0; w < kWavesPerBlock; ++w) {
+            if (wave == w) {
+#pragma unroll
+                for (int kq = 0; kq < HT; ++kq)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float* p = R + (4 * g + r) * RS + 16 * kq + j;
+                        *p = (w == 0 ? 0.f : *p) + gwo[kq][r];
+                    }
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) D[wave * 256 + 64 * q + lane] = gbo[q];
+        __syncthreads();
+        float* dst = a.dwo_partial + (int64_t)bid * a.dwo_p_total;
+        const int mt = a.dwo_m_true, nt = a.dwo_n_true;
+        for (int i = tid; i < 16 * 16 * HT; i += kBlockThreads) {
+            const int o = i / (16 * HT), col = i - o * (16 * HT);
+            if (o < mt && col < nt) dst[a.dwo_w_off + o + mt * col] = R[o * RS + col];
+        }
+        if (a.dwo_b_off >= 0 && tid < mt) {  // db[o]: lanes (g = o / 4, j) of every wave, q = o % 4
+            const int o = tid, q = o & 3, gg = o >> 2;
+            float sum = 0.f;
+            for (int w = 0; w < kWavesPerBlock; ++w)
+                for (int jj = 0; jj < 16; ++jj) sum += D[w * 256 + 64 * q + 16 * gg + jj];
+            dst[a.dwo_b_off + o] = sum;
+        }
+        __syncthreads();  // (the scratch is the next product's staging in a merged launch)
     }
 }
 
@@ -1312,6 +1393,9 @@ hipError_t set_ldense_lds_limit(size_t lds) {
     return hipFuncSetAttribute(reinterpret_cast<void*>(&ldw_kernel<64, 2, 2>), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)ldw_lds_bytes());
 }
+
+bool front_dwo(int mto) { return mto == 1 && DF_FRONT_DWO; }
+size_t front_dwo_lds(int ht) { return front_dwo_lds_bytes(ht); }
 
 hipError_t launch_couple_bwd(int ht, int mto, const LDenseArgs& a, unsigned grid, size_t lds, hipStream_t st) {
     void* k = couple_bwd_ptr(ht, mto);

@@ -665,6 +665,15 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         *ht = DO.bwd.mt;
         *mto = DO.fwd.mt;
         *lds = (size_t)2 * DO.bwd.mt * DO.fwd.mt * 1024;
+        if (front_dwo(DO.fwd.mt)) {  // the output Dense's dW / db come from the front (partial rows: lgrid)
+            a.dwo_partial = t->d_partial;
+            a.dwo_p_total = t->P;
+            a.dwo_w_off = DO.w_off;
+            a.dwo_b_off = DO.b_off;
+            a.dwo_m_true = DO.out_dim;
+            a.dwo_n_true = DO.in_dim;
+            *lds += front_dwo_lds(DO.bwd.mt);
+        }
     };
     // dW = δ · inᵀ, db = Σ δ of every Dense of a net (per-workgroup partials)
     auto dw_args = [&](const SweepOp& op, int par, std::vector<LdwArgs>& out) -> int {
@@ -672,6 +681,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         const int nd = (int)N.dn.size();
         for (int k = 0; k < nd; ++k) {
             const LDense& D = N.dn[k];
+            if (k + 1 == nd && fused_front(op) && front_dwo(D.fwd.mt)) continue;  // (the front's)
             LdwArgs w{};
             w.da = (k + 1 == nd) ? ybuf(par) : dbuf(op, k, par);
             w.lda = W;
@@ -774,7 +784,9 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
                 int ht = 0, mto = 0;
                 size_t lds = 0;
                 front_args(op, par, a, &ht, &mto, &lds);
-                if (e == hipSuccess) e = launch_couple_bwd(ht, mto, a, dgrid, lds, st);
+                // (a front that writes dW partial rows runs on every row's workgroup)
+                const unsigned fgrid = front_dwo(mto) ? (unsigned)t->lgrid : dgrid;
+                if (e == hipSuccess) e = launch_couple_bwd(ht, mto, a, fgrid, lds, st);
             }
             gcur = dbuf(op, nd - 2, par);
             if (fm) {
