@@ -247,6 +247,17 @@ __global__ void __launch_bounds__(train_threads(SPLIT), 1) train_net_kernel(Trai
         for (int i = lane; i < TROWS * kTS; i += 64) TA(t)[i] = 0.f;
     __syncthreads();
 
+    // h̄ = W_outᵀ ȳ on the matrix pipe (DF_TRAIN_HB_MFMA; the SPLIT instances with the
+    // output count at compile time): A = W_out[g][16m + j] (a loop-invariant float per row
+    // tile, 0 for g >= n_af), B = ȳ[g] of sample j — the k = 4 slots are the ≤ 4 outputs
+#ifndef DF_TRAIN_HB_MFMA
+#define DF_TRAIN_HB_MFMA 1
+#endif
+    constexpr bool HBM = SPLIT && NAF > 0 && DF_TRAIN_HB_MFMA;
+    float w3a[HT];
+#pragma unroll
+    for (int m = 0; m < HT; ++m)
+        w3a[m] = (HBM && g < n_af) ? reinterpret_cast<const float*>(fw + N.off_out)[g * INP + 16 * m + j] : 0.f;
     constexpr int NHT = NH ? HT : 1;
     f32x4 gW0[HT], gWo[HT], gWh[NHT][NHT];
     float gb0[HT], gbh[NHT], gbo = 0.f;
@@ -482,6 +493,11 @@ __global__ void __launch_bounds__(train_threads(SPLIT), 1) train_net_kernel(Trai
         f32x4 hb[TT][HT];
 #pragma unroll
         for (int t = 0; t < TT; ++t) {
+            if constexpr (HBM) {  // one v_mfma_f32_16x16x4_f32 per row tile: k = output g of sample j
+                const float bk = g == 0 ? dout[t][0] : g == 1 ? dout[t][1] : g == 2 ? dout[t][2] : dout[t][3];
+#pragma unroll
+                for (int m = 0; m < HT; ++m) hb[t][m] = mfma4(w3a[m], bk, f32x4{0.f, 0.f, 0.f, 0.f});
+            } else {
 #pragma unroll
             for (int m = 0; m < HT; ++m) hb[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -493,6 +509,7 @@ __global__ void __launch_bounds__(train_threads(SPLIT), 1) train_net_kernel(Trai
                         hb[t][m] = hb[t][m] + w * dout[t][k];
                     }
                 }
+            }
             }
             if constexpr (PRE) {
                 const f32x4(&DH)[NP] = NH ? D1 : D0;
