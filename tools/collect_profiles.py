@@ -1,4 +1,4 @@
-"""Copy one measurement pass of tools/gpu_round3.sh (gpurun_out/<tag>/) into profiles/<name>_*:
+"""Copy one measurement pass of tools/gpu_round4.sh (gpurun_out/<tag>/) into profiles/<name>_*:
 bench lines, rocprofv3 kernel-trace summaries and the PMC summaries of the forward and
 training kernels (tools/pmc_summary.py), each PMC file headed by the profiled source sha.
 
@@ -46,7 +46,7 @@ for d, what, kernels in PMC:
     if not os.path.isdir(os.path.join(src, d)):
         continue
     text = [f"# rocprofv3 PMC passes (tools/pmc_sets.txt, one counter set per run), {what}, {label} "
-            f"(tools/gpu_round3.sh)", f"# source sha16 {sha}"]
+            f"(tools/gpu_round4.sh)", f"# source sha16 {sha}"]
     for sub, head in kernels:
         r = subprocess.run([sys.executable, "tools/pmc_summary.py", f"{tag}/{d}", sub],
                            capture_output=True, text=True, check=True)
