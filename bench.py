@@ -51,14 +51,15 @@ TRAFFIC_PROFILES = {"cfg2": os.path.join("profiles", "r05end_pmc_cfg2.txt"),
 
 
 def source_sha16():
-    """sha256 over the HIP/C++ sources of the product library and its header:
-    the PMC summaries record the one they profiled (tools/gpu_pmc_round.sh)."""
+    """sha256 over the HIP/C++ sources of the product library, its header and its
+    Makefile (per-unit compiler flags shape the kernels too): the PMC summaries record
+    the one they profiled (tools/gpu_round4.sh)."""
     import hashlib
 
     h = hashlib.sha256()
     csrc = os.path.join(ROOT, "densityflows.jl_amd", "csrc")
     files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h", ".cpp")))
-    for f in files + ["../../include/densityflows_hip.h"]:
+    for f in files + ["../../include/densityflows_hip.h", "Makefile"]:
         with open(os.path.join(csrc, f), "rb") as fh:
             h.update(f.encode() + b"\0" + fh.read())
     return h.hexdigest()[:16]
