@@ -1,7 +1,9 @@
-// Wide-net kernel variants (df_wide_impl.h): one per chain mode.
+// Wide-net kernel variants (df_wide_impl.h): one per chain mode (MODE_LOGPDF in df_wide_lp.hip).
 #include "df_wide_impl.h"
 
 namespace df {
+
+void* wide_ptr_logpdf(bool split);  // df_wide_lp.hip
 
 namespace {
 template <bool SPLIT>
@@ -10,7 +12,7 @@ void* wide_ptr_t(int mode) {
         case MODE_FWD: return reinterpret_cast<void*>(&wide_kernel<MODE_FWD, SPLIT>);
         case MODE_FWD_INPLACE: return reinterpret_cast<void*>(&wide_kernel<MODE_FWD_INPLACE, SPLIT>);
         case MODE_BWD: return reinterpret_cast<void*>(&wide_kernel<MODE_BWD, SPLIT>);
-        default: return reinterpret_cast<void*>(&wide_kernel<MODE_LOGPDF, SPLIT>);
+        default: return wide_ptr_logpdf(SPLIT);
     }
 }
 void* wide_ptr(int mode, bool split = false) { return split ? wide_ptr_t<true>(mode) : wide_ptr_t<false>(mode); }
