@@ -134,6 +134,8 @@ SIGNATURES = {
     "df_chain_logpdf_sum": (C.c_int, [_VP, _VP, _VP, _VP, _I64, _VP]),
     "df_train_create": (C.c_int, [C.POINTER(_VP), _VP, C.POINTER(df_adam)]),
     "df_train_destroy": (C.c_int, [_VP]),
+    "df_train_create_ex": (C.c_int, [C.POINTER(_VP), _VP, C.POINTER(df_adam), C.c_int]),
+    "df_train_sweep": (C.c_int, [_VP, C.POINTER(C.c_int)]),
     "df_train_num_params": (C.c_int, [_VP, C.POINTER(_I64)]),
     "df_train_gradient": (C.c_int, [_VP, _VP, _VP, _I64, _I64, _VP, _VP]),
     "df_train_grad_ptr": (C.c_int, [_VP, C.POINTER(_VP)]),
@@ -185,7 +187,13 @@ def load(path: str | None = None):
         except OSError as e:  # pragma: no cover - depends on the host
             raise HIPLibraryError(f"cannot load {p}: {e}") from e
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            # a symbol an older build lacks (A/B runs against a saved library) stays
+            # unbound: calling it raises AttributeError; tests/test_host.py checks that the
+            # in-tree build exports every one
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                continue
             fn.restype = res
             fn.argtypes = args
         if lib.df_get_abi_version() != ABI_VERSION:

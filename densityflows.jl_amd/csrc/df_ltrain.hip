@@ -630,7 +630,11 @@ __device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, 
             }
         }
         if constexpr (DWO) {  // dW += ȳ·Hᵀ over the tile's samples (a padding sample's ȳ is 0)
+            // every t_write → tread pair ordered by trn::lds_order (lgkmcnt(0) + a memory
+            // clobber), the training kernel's convention: the reads must follow the writes
+            // and the next rewrite of the transpose rows must follow the reads
             trn::t_write<1>(Ty, dy);
+            trn::lds_order();
 #pragma unroll
             for (int q = 0; q < 4; ++q) gbo[q] += dy[0][q];
             const f32x4 ya = trn::tread(Ty, j, g);  // ȳ[o = j][samples 4g .. 4g + 3]
@@ -638,7 +642,9 @@ __device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, 
             for (int kq = 0; kq < HT; ++kq) {
                 if (kq < a.nkq) {
                     const f32x4 hk[1] = {h[kq]};
+                    trn::lds_order();
                     trn::t_write<1>(Th, hk);
+                    trn::lds_order();
                     const f32x4 hb = trn::tread(Th, j, g);  // H[16kq + j][samples 4g ..]
 #pragma unroll
                     for (int q = 0; q < 4; ++q) gwo[kq] = mfma4(ya[q], hb[q], gwo[kq]);
@@ -893,6 +899,10 @@ __global__ void __launch_bounds__(kLdwSplitThreads, 1) ldw_split_kernel(LdwArgs 
     const int nblk = gridDim.x;
     // sample range of a workgroup: a multiple of the 32-sample step (steps are aligned blocks
     // of the batch, which the H0R relu-mask layout indexes by)
+    // (both instances: the kept-H0 sweep then sums dW1 over the same partition as the
+    // H0-free one, which test_h0_free_sweep_bitwise_equals_kept_h0 relies on; the cost is
+    // at small batches, where up to half the workgroups of the grid get no step: B = 4096
+    // on 256 CUs keeps 128 busy — a few µs per launch at that size)
     const int64_t per = ((a.batch + nblk - 1) / nblk + 31) / 32 * 32;
     const int64_t s_begin = (int64_t)blockIdx.x * per;
     const int64_t s_end = (s_begin + per < a.batch) ? s_begin + per : a.batch;

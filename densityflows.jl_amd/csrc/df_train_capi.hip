@@ -144,11 +144,13 @@ struct df_train {
     // skips the forward recompute.  [(layer·2 + net)·lmax_h + k][B][lwidth]
     float* d_hsave = nullptr;
     bool hsave_on = false;
-    // H0-free sweep (round 5; wide SPLIT chains of relu hidden-256 nets, DF_TRAIN_H0=1 turns it
-    // off): the inverse pass keeps each net's features vcat(θ, u)[axis_nn] ([layer·2 + net][B][32])
+    // H0-free sweep (round 5; wide SPLIT chains of relu hidden-256 nets, DF_SWEEP_H0FREE): the
+    // inverse pass keeps each net's features vcat(θ, u)[axis_nn] ([layer·2 + net][B][32])
     // and H1 only (d_hsave with one slot per net); the split dW1 recomputes H0 from the
     // features and writes its relu mask (d_hmask, 1 KiB per 32 samples) for the W1ᵀδ1 epilogue
     bool fmode = false;
+    int sweep_req = DF_SWEEP_AUTO;   // df_train_create_ex: the requested form (df_sweep_form)
+    bool separate = false;           // DF_SWEEP_SEPARATE: unmerged dW / front launches
     float* d_fsave = nullptr;
     uint32_t* d_hmask = nullptr;
     // repack maps of the chain's wide-kernel blob and biases (plan.wide)
@@ -446,15 +448,16 @@ int build_nets(df_train* t) {
 bool fmode_eligible(const df_train* t) {
     const df_chain* c = t->c;
     const Plan& P = c->plan;
-    auto env1 = [](const char* k) { const char* v = std::getenv(k); return v && v[0] == '1'; };
     if (!t->layerwise || !P.wide || c->no_wide || !use_wsplit(c) || c->exact || P.uniform) return false;
-    if (env1("DF_TRAIN_H0") || env1("DF_TRAIN_NOFUSE") || env1("DF_TRAIN_RECOMPUTE")) return false;
+    if (t->sweep_req != DF_SWEEP_AUTO && t->sweep_req != DF_SWEEP_H0FREE && t->sweep_req != DF_SWEEP_LAYERWISE)
+        return false;
     for (const LNet& N : t->lnets) {
         if (N.pre || N.dn.size() != 3) return false;
         const LDense &D0 = N.dn[0], &D1 = N.dn[1], &D2 = N.dn[2];
         if (D0.act != DF_ACT_RELU || D1.act != DF_ACT_RELU) return false;
         if (D0.in_dim > 32 || D0.out_dim != 256 || D1.in_dim != 256 || D1.out_dim != 256) return false;
-        if (D2.fwd.mt > 2 || D0.bwd.mt > 4 || D1.bwd.sfrag < 0) return false;
+        // (the feature rows the split dW0 / H0 recompute read are 32 floats: 16 · bwd.mt <= 32)
+        if (D2.fwd.mt > 2 || D0.bwd.mt > 2 || D1.bwd.sfrag < 0) return false;
     }
     return true;
 }
@@ -498,18 +501,32 @@ int ensure_capacity(df_train* t, int64_t batch) {
         // keep the inverse pass's hidden activations when the chain runs on the generic
         // kernel and they fit (else the sweep recomputes them)
         t->hsave_on = false;
-        if (!P.uniform && !(std::getenv("DF_TRAIN_RECOMPUTE") && std::getenv("DF_TRAIN_RECOMPUTE")[0] == '1')) {
-            // fmode: H1 only, plus the 32-float feature rows and the relu-mask buffer
-            const size_t hbytes = row * (size_t)P.n_layers * 2 * (t->fmode ? 1 : t->lmax_h);
-            const size_t fbytes = t->fmode ? sizeof(float) * (size_t)cap * 32 * P.n_layers * 2 : 0;
+        if (!P.uniform && t->sweep_req != DF_SWEEP_RECOMPUTE) {
+            // fmode: H1 only, plus the 32-float feature rows and the relu-mask buffer; else
+            // H0 and H1 of every net.  Whatever does not fit falls back: fmode → kept H0/H1
+            // → recompute (the sweep's forms, struct df_train)
             size_t free_b = 0, total_b = 0;
-            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && hbytes + fbytes < free_b / 2 &&
-                hipMalloc(reinterpret_cast<void**>(&t->d_hsave), hbytes) == hipSuccess) {
-                t->hsave_on = true;
-                if (t->fmode && (hipMalloc(reinterpret_cast<void**>(&t->d_fsave), fbytes) != hipSuccess ||
-                                 hipMalloc(reinterpret_cast<void**>(&t->d_hmask), (size_t)(cap + 31) / 32 * 1024) != hipSuccess))
-                    return set_err(DF_ERR_NOMEM, "hipMalloc failed (training feature snapshots)");
-            }
+            const bool info = hipMemGetInfo(&free_b, &total_b) == hipSuccess;
+            auto try_keep = [&](bool fm) {
+                const size_t hbytes = row * (size_t)P.n_layers * 2 * (fm ? 1 : t->lmax_h);
+                const size_t fbytes = fm ? sizeof(float) * (size_t)cap * 32 * P.n_layers * 2 : 0;
+                const size_t mbytes = fm ? (size_t)(cap + 31) / 32 * 1024 : 0;
+                if (!info || hbytes + fbytes + mbytes >= free_b / 2) return false;
+                if (hipMalloc(reinterpret_cast<void**>(&t->d_hsave), hbytes) == hipSuccess &&
+                    (!fm || (hipMalloc(reinterpret_cast<void**>(&t->d_fsave), fbytes) == hipSuccess &&
+                             hipMalloc(reinterpret_cast<void**>(&t->d_hmask), mbytes) == hipSuccess)))
+                    return true;
+                for (float** p : {&t->d_hsave, &t->d_fsave})
+                    if (*p) {
+                        (void)hipFree(*p);
+                        *p = nullptr;
+                    }
+                if (t->d_hmask) (void)hipFree(t->d_hmask);
+                t->d_hmask = nullptr;
+                return false;
+            };
+            if (t->fmode && !try_keep(true)) t->fmode = false;  // sized for H0 and H1 below
+            if (t->fmode || try_keep(false)) t->hsave_on = true;
             (void)hipGetLastError();
         }
         for (int k = 0; k <= t->lmax_h; ++k) {
@@ -623,8 +640,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
         b.ld_in = b.ld_out = b.ld_h = b.ld_x = W;
         return b;
     };
-    const bool no_fuse = std::getenv("DF_TRAIN_NOFUSE") && std::getenv("DF_TRAIN_NOFUSE")[0] == '1';
-    const bool no_merge = std::getenv("DF_TRAIN_NOMERGE") && std::getenv("DF_TRAIN_NOMERGE")[0] == '1';
+    const bool no_merge = t->separate;  // DF_SWEEP_SEPARATE
     auto keeps = [&](const SweepOp& op) { return t->hsave_on && !t->lnets[op.net].pre; };
     const bool fm = t->fmode && t->hsave_on && t->d_fsave;  // H0-free sweep (struct df_train)
     auto net_slot = [&](const SweepOp& op) { return 2 * op.layer + (op.phase == TR_PHASE_T ? 1 : 0); };
@@ -633,7 +649,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
     auto fused_front = [&](const SweepOp& op) {
         const LNet& N = t->lnets[op.net];
         const int nd = (int)N.dn.size();
-        return nd >= 2 && keeps(op) && N.dn[nd - 1].fwd.mt <= 2 && N.dn[0].bwd.mt <= 4 && !no_fuse;
+        return nd >= 2 && keeps(op) && N.dn[nd - 1].fwd.mt <= 2 && N.dn[0].bwd.mt <= 4;
     };
     // H_k of a net: kept by the inverse pass, or recomputed into the shared buffers
     auto Hbuf = [&](const SweepOp& op, int k) -> float* {
@@ -797,6 +813,7 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
                         break;
                     }
             }
+            bool xbar_apart = false;  // x̄ = W0ᵀδ0 as its own product (a wide first Dense)
             for (int k = nd - 2; k >= 1; --k) {
                 LDenseArgs c2 = b;
                 c2.in = gcur;
@@ -821,19 +838,34 @@ int lsweep(df_train* t, const float* x, const float* theta, int64_t batch, float
                     const size_t wbytes = c2.sfrag ? (size_t)(lo.nkq / 2 > 1 ? 2 : 1) * lo.mt * 3072
                                                    : (size_t)(nchunks > 1 ? 2 : 1) * std::min(lo.nkq, lo.chunk_kq) *
                                                          lo.mt * 1024;
-                    const size_t w0b = c2.w0s ? (size_t)(c2.w0t_nkq / 2) * c2.w0t_mt * 3072
-                                              : (size_t)c2.w0t_mt * c2.w0t_nkq * 1024;
-                    const size_t lds2 = wbytes + w0b + 64;  // + z̄ column table
+                    auto w0_bytes = [&]() {
+                        return c2.w0s ? (size_t)(c2.w0t_nkq / 2) * c2.w0t_mt * 3072
+                                      : (size_t)c2.w0t_mt * c2.w0t_nkq * 1024;
+                    };
+                    // W0ᵀ stays resident beside the W1ᵀ chunk buffers: with more than 32
+                    // conditioner inputs its split planes (or even its f32 fragments, at 64
+                    // inputs) do not fit; then the f32 fragments, or x̄ = W0ᵀδ0 as its own
+                    // product after the δ0 kernel
+                    constexpr size_t kLdsMax = 160 * 1024;
+                    if (wbytes + w0_bytes() + 64 > kLdsMax) c2.w0s = nullptr;
+                    const size_t lds2 = wbytes + w0_bytes() + 64;  // + z̄ column table
                     c2.wfrag = lb + lo.frag;
                     c2.nkq = lo.nkq;
                     c2.chunk_kq = lo.chunk_kq;
-                    if (e == hipSuccess) e = launch_ldense(lo.mt, LIN_BUF, xepi, c2, dgrid, lds2, st);
+                    if (lds2 <= kLdsMax) {
+                        if (e == hipSuccess) e = launch_ldense(lo.mt, LIN_BUF, xepi, c2, dgrid, lds2, st);
+                    } else {
+                        if (fm) return set_err(DF_ERR_INVALID, "internal: H0-free sweep with a wide first Dense");
+                        c2.w0t = nullptr;
+                        dense(lo, LIN_BUF, LEPI_DACT, c2);
+                        xbar_apart = true;
+                    }
                 } else {
                     dense(N.dn[k].bwd, LIN_BUF, LEPI_DACT, c2);
                 }
                 gcur = dbuf(op, k - 1, par);
             }
-            if (nd == 2) {
+            if (nd == 2 || xbar_apart) {
                 LDenseArgs c3 = b;
                 c3.in = gcur;
                 dense(N.dn[0].bwd, LIN_BUF, LEPI_XBAR, c3);
@@ -922,11 +954,22 @@ int df_train_destroy(df_train* t) {
 }
 
 int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
+    return df_train_create_ex(out, c, opt, DF_SWEEP_AUTO);
+}
+
+int df_train_create_ex(df_train** out, df_chain* c, const df_adam* opt, int sweep) {
     if (!out || !c) return set_err(DF_ERR_INVALID, "null pointer");
     *out = nullptr;
+    const int form = sweep & ~DF_SWEEP_SEPARATE;
+    if (form < DF_SWEEP_AUTO || form > DF_SWEEP_LAYERWISE || (sweep & ~(DF_SWEEP_SEPARATE | 7)))
+        return set_err(DF_ERR_INVALID, "unknown sweep form");
+    if (form == DF_SWEEP_FUSED && (sweep & DF_SWEEP_SEPARATE))
+        return set_err(DF_ERR_INVALID, "DF_SWEEP_SEPARATE applies to the layer-wise forms");
     df_train* t = new (std::nothrow) df_train();
     if (!t) return set_err(DF_ERR_NOMEM, "host allocation failed");
     t->c = c;
+    t->sweep_req = form;
+    t->separate = (sweep & DF_SWEEP_SEPARATE) != 0;
     t->opt = opt ? *opt : df_adam{1e-3f, 0.9f, 0.999f, 1e-8f};
     if (!(t->opt.eta >= 0.f) || !(t->opt.beta1 >= 0.f && t->opt.beta1 < 1.f) ||
         !(t->opt.beta2 >= 0.f && t->opt.beta2 < 1.f) || !(t->opt.epsilon >= 0.f)) {
@@ -939,9 +982,8 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
     for (const DevDense& D : P.denses)
         if (act_needs_pre(D.act) && !P.relu_only) t->amode = trn::AM_PRE;
     // fused per-net kernel when every conditioner fits its registers, else layer-wise
-    const char* force = std::getenv("DF_TRAIN_LAYERWISE");
-    int rc = (force && force[0] == '1') ? DF_ERR_UNSUPPORTED : build_nets(t);
-    if (rc == DF_ERR_UNSUPPORTED) {
+    int rc = (form == DF_SWEEP_AUTO || form == DF_SWEEP_FUSED) ? build_nets(t) : DF_ERR_UNSUPPORTED;
+    if (rc == DF_ERR_UNSUPPORTED && form != DF_SWEEP_FUSED) {
         t->nets.clear();
         t->net_nh.clear();
         t->ops.clear();
@@ -994,10 +1036,16 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
         t->lgrid = std::max(1, c->n_cu);
         t->grid = t->lgrid;  // partial rows
         t->fmode = fmode_eligible(t);
+        // an explicit form the chain cannot take: the H0-free sweep's shape, or kept
+        // activations of a chain whose inverse pass (the specialised kernel) keeps none
+        if ((form == DF_SWEEP_H0FREE && !t->fmode) || (form == DF_SWEEP_KEPT && P.uniform)) {
+            df_train_destroy(t);
+            return set_err(DF_ERR_UNSUPPORTED, form == DF_SWEEP_H0FREE
+                                                   ? "DF_SWEEP_H0FREE needs wide SPLIT nets Dense(<=32,256,relu), "
+                                                     "Dense(256,256,relu), Dense(256,<=32)"
+                                                   : "DF_SWEEP_KEPT needs a chain on the generic or wide kernel");
+        }
     }
-    if (const char* dbg = std::getenv("DF_TRAIN_DEBUG"); dbg && dbg[0] == '1')  // diagnostic: the sweep's form
-        std::fprintf(stderr, "[df] trainer: %s%s\n", t->layerwise ? "layer-wise" : "fused",
-                     t->layerwise ? (t->fmode ? ", H0-free sweep (features + H1 kept)" : ", H0/H1 kept or recomputed") : "");
     const size_t pb = sizeof(float) * (size_t)std::max<int64_t>(t->P, 4);
     if (hipMalloc(reinterpret_cast<void**>(&t->d_params), pb) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&t->d_m), pb) != hipSuccess ||
@@ -1047,6 +1095,18 @@ int df_train_create(df_train** out, df_chain* c, const df_adam* opt) {
 int df_train_num_params(const df_train* t, int64_t* count) {
     if (!t || !count) return set_err(DF_ERR_INVALID, "null pointer");
     *count = t->P;
+    return DF_OK;
+}
+
+int df_train_sweep(const df_train* t, int* form) {
+    if (!t || !form) return set_err(DF_ERR_INVALID, "null pointer");
+    if (!t->layerwise) *form = DF_SWEEP_FUSED;
+    else if (t->cap == 0)  // no gradient yet: the form ensure_capacity will try first
+        *form = t->fmode ? DF_SWEEP_H0FREE
+                         : (t->c->plan.uniform || t->sweep_req == DF_SWEEP_RECOMPUTE) ? DF_SWEEP_RECOMPUTE : DF_SWEEP_KEPT;
+    else if (t->fmode && t->hsave_on && t->d_fsave) *form = DF_SWEEP_H0FREE;
+    else *form = t->hsave_on ? DF_SWEEP_KEPT : DF_SWEEP_RECOMPUTE;
+    if (t->layerwise && t->separate) *form |= DF_SWEEP_SEPARATE;
     return DF_OK;
 }
 

@@ -391,7 +391,17 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 #endif
 template <int S>
 __device__ __forceinline__ float split_rem(bf16x2 h, float x) {
-#if DF_SPLIT_DOT2
+#if DF_SPLIT_DOT2 == 2
+    // plain VALU: hi unpacked by a shift (low half) or a mask (high half), then one
+    // v_sub_f32 (asm: -O3 would pair two of them into v_pk_add_f32).  Beside MFMAs a
+    // v_dot2c_f32_bf16 or a packed f32 op waits for the matrix pipe (≈ 16 cycles each,
+    // tools/probe/mfma_valu.hip); shifts, masks and subtracts co-issue.
+    const uint32_t u = __builtin_bit_cast(uint32_t, h);
+    const float hi = __uint_as_float(S == 0 ? (u << 16) : (u & 0xffff0000u));
+    float r;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(hi));
+    return r;
+#elif DF_SPLIT_DOT2
     // (-1, 0) is materialised by a v_mov: the compiler would otherwise encode it as the
     // inline constant -1.0, which the hardware reads as the f32 0xbf800000, i.e. (0, -1)
     // (probe: tools/probe/dot2_split.hip).  The asm is pure, so it is hoisted and shared.

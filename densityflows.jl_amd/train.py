@@ -49,16 +49,31 @@ class _DeviceArray:
                                          "version": 2, "strides": None}
 
 
-class HIPTrainer:
-    """A ``df_train`` handle bound to a compiled chain (one device)."""
+# reverse-sweep forms (df_sweep_form, include/densityflows_hip.h)
+SWEEP_AUTO, SWEEP_FUSED, SWEEP_H0FREE, SWEEP_KEPT, SWEEP_RECOMPUTE, SWEEP_LAYERWISE = 0, 1, 2, 3, 4, 5
+SWEEP_SEPARATE = 16
+# the form a HIPTrainer requests when none is given (tests set it to exercise one path
+# through code that builds its own trainers, e.g. train_)
+DEFAULT_SWEEP = SWEEP_AUTO
+SWEEP_NAMES = {SWEEP_FUSED: "fused", SWEEP_H0FREE: "h0free", SWEEP_KEPT: "kept", SWEEP_RECOMPUTE: "recompute"}
 
-    def __init__(self, chain: HIPChain, opt: Adam):
+
+class HIPTrainer:
+    """A ``df_train`` handle bound to a compiled chain (one device).  ``sweep``: a
+    df_sweep_form to request (default: the library picks, SWEEP_AUTO)."""
+
+    def __init__(self, chain: HIPChain, opt: Adam, sweep: int | None = None):
         self.chain = chain  # keeps the df_chain alive for this handle's lifetime
         self.lib = chain.lib
         self.opt = opt
         h = C.c_void_p()
         a = _lib.df_adam(opt.eta, opt.beta[0], opt.beta[1], opt.epsilon)
-        _lib.check(self.lib.df_train_create(C.byref(h), chain.handle, C.byref(a)), "df_train_create")
+        sweep = DEFAULT_SWEEP if sweep is None else sweep
+        if sweep == SWEEP_AUTO and not hasattr(self.lib, "df_train_create_ex"):  # a pre-ABI-5 build (A/B runs)
+            _lib.check(self.lib.df_train_create(C.byref(h), chain.handle, C.byref(a)), "df_train_create")
+        else:
+            _lib.check(self.lib.df_train_create_ex(C.byref(h), chain.handle, C.byref(a), int(sweep)),
+                       "df_train_create_ex")
         self.handle = h
         n = C.c_int64()
         _lib.check(self.lib.df_train_num_params(self.handle, C.byref(n)))
@@ -104,6 +119,12 @@ class HIPTrainer:
         _lib.check(self.lib.df_train_step_graph(self.handle, _ptr(xbuf), _ptr(thbuf), C.c_int64(batch),
                                                 C.c_int64(n_total), _ptr(lpsum), _stream(self.device)),
                    "df_train_step_graph")
+
+    def sweep(self) -> int:
+        """The reverse-sweep form this trainer runs (df_train_sweep: SWEEP_* | SWEEP_SEPARATE)."""
+        f = C.c_int()
+        _lib.check(self.lib.df_train_sweep(self.handle, C.byref(f)), "df_train_sweep")
+        return int(f.value)
 
     def set_debug(self, on: bool = True) -> None:
         """train!(...; debug=true): refuse the Adam update of a non-finite loss

@@ -258,6 +258,38 @@ typedef struct df_adam {
 /* Optimisers.setup(Adam(...), flow.model): state m = v = 0, βᵗ = β. */
 int df_train_create(df_train** out, df_chain* chain, const df_adam* opt);
 int df_train_destroy(df_train* t);
+/* Form of the reverse sweep behind df_train_gradient.  Every form
+ * computes the same gradient (rrule(RNVP_backward), src/affine/RNVP.jl:99-147, through
+ * Flux.gradient, src/Flows.jl:398-411); df_train_create picks one from the chain:
+ *   DF_SWEEP_FUSED      one fused per-net kernel: every conditioner the default
+ *                       _dflt_net shape at hidden <= 64, <= 4 transformed dims;
+ *   DF_SWEEP_H0FREE     layer-wise; the inverse pass keeps each net's features and H1,
+ *                       the split dW1 recomputes H0: wide SPLIT chains whose nets are all
+ *                       Dense(<= 32, 256, relu) → Dense(256, 256, relu) → Dense(256, <= 32);
+ *   DF_SWEEP_KEPT       layer-wise; the inverse pass keeps every hidden activation
+ *                       (chains on the generic or wide kernels, when they fit in half the
+ *                       free device memory);
+ *   DF_SWEEP_RECOMPUTE  layer-wise; the sweep recomputes the hidden activations.
+ * H0FREE → KEPT → RECOMPUTE is also the fallback order when device memory runs short
+ * (decided at the first gradient of each batch capacity). */
+typedef enum df_sweep_form {
+    DF_SWEEP_AUTO = 0,
+    DF_SWEEP_FUSED = 1,
+    DF_SWEEP_H0FREE = 2,
+    DF_SWEEP_KEPT = 3,
+    DF_SWEEP_RECOMPUTE = 4,
+    /* request only: any layer-wise form (the library picks among the three above) */
+    DF_SWEEP_LAYERWISE = 5,
+    /* flag (with a layer-wise form): each net's dW products and the next net's
+     * backward front as separate launches instead of merged ones (the same sums in
+     * the same order: a bitwise A/B reference for the merged launches) */
+    DF_SWEEP_SEPARATE = 16
+} df_sweep_form;
+/* df_train_create with a requested sweep form (DF_SWEEP_AUTO: as df_train_create).
+ * A form the chain cannot take returns DF_ERR_UNSUPPORTED. */
+int df_train_create_ex(df_train** out, df_chain* chain, const df_adam* opt, int sweep);
+/* The form the trainer runs (before its first gradient: the one it will try first). */
+int df_train_sweep(const df_train* t, int* form);
 /* Number of trainable parameters (length of the flat vectors below). */
 int df_train_num_params(const df_train* t, int64_t* count);
 /* How the trainer's entry points (df_train_gradient and every step built on

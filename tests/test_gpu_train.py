@@ -16,6 +16,7 @@ import pytest
 
 import densityflows_amd as dfa
 from densityflows_amd.train import Adam, HIPTrainer, load_trainables, setup, train_, trainables
+import densityflows_amd.train as train_mod
 from helpers import _single_dense_spec, random_net, close, spec_to_element
 from oracle import flow_oracle as O
 
@@ -120,11 +121,11 @@ SPECS = {"readme": (_readme_spec, 5, 1), "cfg2": (_cfg2_spec, 5, 0), "mixed": (_
 
 @pytest.fixture(params=["fused", "layerwise"])
 def path(request, monkeypatch):
-    """Both training paths: the fused per-net kernel and the layer-wise GEMMs."""
-    if request.param == "layerwise":
-        monkeypatch.setenv("DF_TRAIN_LAYERWISE", "1")
-    else:
-        monkeypatch.delenv("DF_TRAIN_LAYERWISE", raising=False)
+    """Both training paths: the fused per-net kernel (when the chain takes it) and the
+    layer-wise GEMMs, requested through df_train_create_ex (train.DEFAULT_SWEEP is the
+    form every HIPTrainer built without an explicit one asks for)."""
+    monkeypatch.setattr(train_mod, "DEFAULT_SWEEP",
+                        train_mod.SWEEP_LAYERWISE if request.param == "layerwise" else train_mod.SWEEP_AUTO)
     return request.param
 
 
@@ -198,11 +199,10 @@ def test_gradient_parity_exact_f32(cuda, monkeypatch, name, B):
 def test_gradient_parity_layerwise_wide(cuda, monkeypatch, name, B, recompute):
     """Conditioners beyond the fused kernel (hidden 128/256, 3 hidden Denses, MFMA
     outputs): the layer-wise path is selected automatically.  By default the
-    inverse pass keeps the hidden activations; DF_TRAIN_RECOMPUTE=1 recomputes them."""
-    if recompute:
-        monkeypatch.setenv("DF_TRAIN_RECOMPUTE", "1")
-    else:
-        monkeypatch.delenv("DF_TRAIN_RECOMPUTE", raising=False)
+    inverse pass keeps the hidden activations (config 5: its features and H1);
+    DF_SWEEP_RECOMPUTE recomputes them."""
+    monkeypatch.setattr(train_mod, "DEFAULT_SWEEP",
+                        train_mod.SWEEP_RECOMPUTE if recompute else train_mod.SWEEP_AUTO)
     test_gradient_parity(cuda, "layerwise", name, B)
 
 
@@ -210,37 +210,80 @@ def test_gradient_parity_layerwise_wide(cuda, monkeypatch, name, B, recompute):
 def test_merged_sweep_bitwise_equals_separate_launches(cuda, monkeypatch, name, B):
     """The merged sweep launches (net i's dW products beside net i+1's output-Dense /
     pullback front, sweep_kernel) compute bitwise the gradient of the separate
-    couple_bwd / ldw launches (DF_TRAIN_NOMERGE=1): same sums in the same order."""
+    couple_bwd / ldw launches (DF_SWEEP_SEPARATE): same sums in the same order."""
     spec, chain, d, n = _setup(name)
     x, th = _inputs(d, n, B)
     out = []
-    for nomerge in ("0", "1"):
-        monkeypatch.setenv("DF_TRAIN_NOMERGE", nomerge)
-        tr = HIPTrainer(spec_to_element(spec).hip(), Adam())
+    for sweep in (train_mod.SWEEP_AUTO, train_mod.SWEEP_LAYERWISE | train_mod.SWEEP_SEPARATE):
+        tr = HIPTrainer(spec_to_element(spec).hip(), Adam(), sweep=sweep)
+        assert bool(tr.sweep() & train_mod.SWEEP_SEPARATE) == (sweep != train_mod.SWEEP_AUTO)
         out.append(_gpu_grad(tr, x, th, cuda))
     np.testing.assert_array_equal(out[0][0], out[1][0])
     assert out[0][1] == out[1][1]
 
 
 @pytest.mark.parametrize("B", [5, 300, 777, 3001])
-def test_h0_free_sweep_bitwise_equals_kept_h0(cuda, monkeypatch, capfd, B):
+def test_h0_free_sweep_bitwise_equals_kept_h0(cuda, B):
     """Config-5 nets (wide SPLIT inverse, relu hidden-256): the default sweep keeps the
     features and H1 only and recomputes H0 inside the split dW1 (with its relu mask for
     the W1ᵀδ1 epilogue).  The recompute is the inverse pass's own first-Dense
     arithmetic, so the gradient and Σ logpdf are bitwise those of the sweep that keeps
-    H0 (DF_TRAIN_H0=1); batches below / across the 32-sample dW steps included."""
+    H0 (DF_SWEEP_KEPT); batches below / across the 32-sample dW steps included."""
     spec, chain, d, n = _setup("cfg5")
     x, th = _inputs(d, n, B)
     out = []
-    monkeypatch.setenv("DF_TRAIN_DEBUG", "1")
-    for keep_h0 in ("0", "1"):
-        monkeypatch.setenv("DF_TRAIN_H0", keep_h0)
-        tr = HIPTrainer(spec_to_element(spec).hip(), Adam())
-        err = capfd.readouterr().err
-        assert ("H0-free sweep" in err) == (keep_h0 == "0"), err
+    for sweep in (train_mod.SWEEP_AUTO, train_mod.SWEEP_KEPT):
+        tr = HIPTrainer(spec_to_element(spec).hip(), Adam(), sweep=sweep)
+        want = train_mod.SWEEP_H0FREE if sweep == train_mod.SWEEP_AUTO else train_mod.SWEEP_KEPT
+        assert tr.sweep() == want
         out.append(_gpu_grad(tr, x, th, cuda))
+        assert tr.sweep() == want  # after the first gradient: the buffers fitted
     np.testing.assert_array_equal(out[0][0], out[1][0])
     assert out[0][1] == out[1][1]
+
+
+def _cfg5_in40_spec(rng):
+    """config-5-sized nets whose first Dense takes 40 inputs (d = 32, n = 24): the wide
+    SPLIT kernel runs the inverse pass, but the H0-free sweep's 32-float feature rows do
+    not hold them."""
+    return {"kind": "chain", "layers": [
+        O.coupling_block(rng, O.coupling_axes_cut(32, n=24), hidden=256, bias_scale=0.1, out_scale=0.1)
+        for _ in range(2)]}
+
+
+SPECS["cfg5_in40"] = (_cfg5_in40_spec, 32, 24)
+
+
+@pytest.mark.parametrize("name,sweep,want", [
+    ("readme", "AUTO", "FUSED"), ("cfg2", "AUTO", "FUSED"), ("mixed", "AUTO", "FUSED"),
+    ("readme", "LAYERWISE", "RECOMPUTE"), ("cfg2", "LAYERWISE", "RECOMPUTE"),
+    ("wide", "AUTO", "KEPT"), ("wide", "RECOMPUTE", "RECOMPUTE"),
+    ("cfg5", "AUTO", "H0FREE"), ("cfg5", "LAYERWISE", "H0FREE"), ("cfg5", "KEPT", "KEPT"),
+    ("cfg5", "RECOMPUTE", "RECOMPUTE"), ("cfg5_in40", "AUTO", "KEPT"),
+    ("cfg5", "FUSED", None), ("wide", "H0FREE", None), ("cfg5_in40", "H0FREE", None), ("cfg2", "KEPT", None)])
+def test_sweep_form_per_shape(cuda, name, sweep, want):
+    """Which reverse sweep each conditioner shape takes (df_train_sweep):
+    one production form per shape class, and an explicit request the shape cannot take
+    is refused (DF_ERR_UNSUPPORTED) rather than silently served by another form.  The
+    form reported before the first gradient is the one the gradient runs (the buffers
+    of these batches fit), and the gradient matches the oracle."""
+    spec, chain, d, n = _setup(name)
+    req = getattr(train_mod, "SWEEP_" + sweep)
+    if want is None:
+        with pytest.raises(dfa._lib.UnsupportedError):
+            HIPTrainer(chain.hip(), Adam(), sweep=req)
+        return
+    tr = HIPTrainer(chain.hip(), Adam(), sweep=req)
+    assert tr.sweep() == getattr(train_mod, "SWEEP_" + want)
+    B = 300
+    x, th = _inputs(d, n, B)
+    g, lpsum = _gpu_grad(tr, x, th, cuda)
+    assert tr.sweep() == getattr(train_mod, "SWEEP_" + want)
+    loss, ref = O.nll_and_grad(spec, x, th if n else np.zeros((0, B)))
+    ref = _flat_oracle_grads(spec, ref)
+    assert abs(-lpsum / B - loss) <= 1e-5 * max(1.0, abs(loss))
+    for sl in _tensor_slices(spec):
+        assert close(g[sl], ref[sl], G_RTOL, G_ATOL)[0]
 
 
 @pytest.mark.parametrize("name", ["cfg2", "wide"])
@@ -520,14 +563,15 @@ def test_gradient_parity_edge_cases(cuda, path, name, B):
     test_gradient_parity(cuda, path, name, B)
 
 
-@pytest.mark.parametrize("name", ["readme", "cfg2", "mixed"])
+@pytest.mark.parametrize("name", ["readme", "cfg2", "mixed", "cfg5"])
 def test_step_graph_matches_eager_steps(cuda, path, name):
     """df_train_step_graph (eager on first sight of its buffers, captured on the
     second, replayed after) leaves bitwise the parameters of the same sequence of
     eager df_train_step calls: same kernels, Adam's βᵗ advanced on the device.
     The sequence changes batch size (a new graph), grows the batch past the
     trainer's capacity (buffers reallocated: the old capture is dropped) and
-    comes back to the first buffers."""
+    comes back to the first buffers.  Config 5 runs the H0-free sweep, whose feature
+    rows, relu masks and partial rows are reallocated by that growth."""
     import torch
 
     spec, chain, d, n = _setup(name, seed=7)

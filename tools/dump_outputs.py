@@ -2,8 +2,8 @@
 seeded inputs, for bitwise A/B comparisons between builds:
     python tools/dump_outputs.py out.npz         # one build
     python tools/dump_outputs.py --compare a.npz b.npz
-Workloads: the bench's config-2 and config-4 models (forward, inverse, logpdf) and one
-config-2 training gradient."""
+Workloads: the bench's config-2 and config-4 models (forward, inverse, logpdf) and a
+training gradient of each (config 4's is the config-5 sweep)."""
 import os
 import sys
 
@@ -38,12 +38,11 @@ def dump(path):
         hc.run_logpdf(x, th, lp, B)
         for k, v in (("x", x), ("ldj", ldj), ("zb", zb), ("ldjb", ldjb), ("lp", lp)):
             out[f"{cfg}_{k}"] = v.cpu().numpy()
-        if cfg == "cfg2":
-            tr = HIPTrainer(hc, Adam(1e-3))
-            tr.gradient(x, th, B, B)
-            torch.cuda.synchronize()
-            out["cfg2_grad"] = tr.grad().cpu().numpy()
-            del tr
+        tr = HIPTrainer(hc, Adam(1e-3))  # cfg4: the config-5 sweep (wide inverse pass)
+        tr.gradient(x, th, B, B)
+        torch.cuda.synchronize()
+        out[f"{cfg}_grad"] = tr.grad().cpu().numpy()
+        del tr
     np.savez(path, **out)
     print("dumped", path, {k: v.shape for k, v in out.items()})
 
