@@ -69,30 +69,26 @@ struct WStager {
     int bytes;  // ring slot size: kWideStageBytes, or kWideSplitStageBytes (SPLIT)
     int nb;     // ring slots: kWideBufs, or kWideSplitBufs (SPLIT)
     // staggered DMA (SPLIT): this wave's pieces of the next stage, issued one per
-    // m-tile by split_chunk instead of all at the stage switch.  The cursor is wave-uniform
-    // and advanced by a constant per piece: a piece costs an SGPR-pair add, an M0 add and a
-    // compare-and-branch among the MFMAs (recomputing the 64-bit address from the piece
-    // index took ~13 scalar instructions per m-tile, more than an MFMA gap hides)
+    // m-tile by split_chunk instead of all at the stage switch
     const uint8_t* blob;
-    const uint8_t* pg;  // global address of this wave's next piece of the pending stage
-    uint8_t* pl;        // its LDS destination
-    int pleft;          // pieces this wave still has to issue
+    int psrc;   // byte offset of the pending stage in the blob
+    int pdst;   // its ring slot's byte offset from base
+    int pnext, pend;
     __device__ __forceinline__ uint8_t* buf() const { return slot(idx); }
     __device__ __forceinline__ uint8_t* slot(int i) const { return base + (i % nb) * bytes; }
     template <int NW>
     __device__ __forceinline__ void issue_one() {
-        if (pleft > 0) {
+        if (pnext < pend) {
             const int lane = threadIdx.x & 63;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(pg + lane * 16),
-                                             (__attribute__((address_space(3))) void*)pl, 16, 0, 0);
-            pg += NW << 10;
-            pl += NW << 10;
-            --pleft;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(blob + psrc + (pnext << 10) + lane * 16),
+                                             (__attribute__((address_space(3))) void*)(base + pdst + (pnext << 10)), 16,
+                                             0, 0);
+            pnext += NW;
         }
     }
     template <int NW>
     __device__ __forceinline__ void issue_all() {
-        while (pleft > 0) issue_one<NW>();
+        while (pnext < pend) issue_one<NW>();
     }
 };
 
@@ -177,10 +173,10 @@ __device__ __forceinline__ void ensure(int s, WStager& sg, const ChainArgs& a) {
     if (nidx + NB - 1 < sg.n) {
         if (STAGGER) {
             const DevStage& st = cref(a.stages + cref(sg.sched + nidx + NB - 1));
-            const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-            sg.pg = sg.blob + st.src_off + (wave << 10);
-            sg.pl = sg.slot(nidx + NB - 1) + (wave << 10);
-            sg.pleft = dma_ops<NW>(st.bytes, wave);
+            sg.psrc = (int)st.src_off;
+            sg.pdst = (int)(sg.slot(nidx + NB - 1) - sg.base);
+            sg.pnext = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            sg.pend = st.bytes >> 10;
         } else {
             dma<NW>(a, cref(sg.sched + nidx + NB - 1), sg.slot(nidx + NB - 1));
         }
@@ -633,9 +629,7 @@ __global__ void __launch_bounds__(SPLIT ? wide::kSplitWaves * 64 : wide::kThread
     sg.bytes = SBYTES;
     sg.nb = NB;
     sg.blob = a.blob;
-    sg.pg = a.blob;
-    sg.pl = smem;
-    sg.pleft = 0;
+    sg.psrc = sg.pdst = sg.pnext = sg.pend = 0;
     for (int q = 0; q < NB - 1 && q < sg.n; ++q) dma<NW>(a, cref(sg.sched + q), sg.slot(q));
 
     for (int i = tid; i < a.tab_ints; i += NT) tab[i] = a.tables[i];

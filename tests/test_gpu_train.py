@@ -578,8 +578,10 @@ def test_step_graph_matches_eager_steps(cuda, path, name):
     chain2 = spec_to_element(spec)    # a trainer repacks its chain's weights: one chain each
     eager = HIPTrainer(chain.hip(device=cuda.index or 0), Adam(1e-3))
     graph = HIPTrainer(chain2.hip(device=cuda.index or 0), Adam(1e-3))
+    seq = (64, 64, 64, 64, 33, 33, 33, 64, 5000, 5000, 5000, 64, 64)
     bufs = {}
-    for B in (64, 64, 64, 64, 33, 33, 33, 64, 5000, 5000, 5000, 64, 64):
+    hist = []
+    for i, B in enumerate(seq):
         x, th = _inputs(d, n, B, seed=B)
         xd, td = _dev(x, cuda), (_dev(th, cuda) if n else None)
         if B not in bufs:                       # persistent staging buffers per batch size
@@ -591,7 +593,21 @@ def test_step_graph_matches_eager_steps(cuda, path, name):
         eager.step(xd, td, B)
         graph.step_graph(xs, ts, B)
         torch.cuda.synchronize()
-        np.testing.assert_array_equal(graph.get_params(), eager.get_params())
+        pe, pg = eager.get_params(), graph.get_params()
+        hist.append(pe.copy())
+        if not np.array_equal(pg, pe):
+            # which one is off: replay the sequence up to here on a third, eager trainer
+            ref = HIPTrainer(spec_to_element(spec).hip(device=cuda.index or 0), Adam(1e-3))
+            for k, Bk in enumerate(seq[:i + 1]):
+                xk, tk = _inputs(d, n, Bk, seed=Bk)
+                ref.step(_dev(xk, cuda), _dev(tk, cuda) if n else None, Bk)
+                torch.cuda.synchronize()
+                pr = ref.get_params()
+                if not np.array_equal(pr, hist[k]):
+                    break
+            pytest.fail(f"step {i} (B = {B}): graph and eager parameters differ; a third eager replay "
+                        f"{'matches the eager trainer' if np.array_equal(pr, pe) else 'matches the graph trainer' if np.array_equal(pr, pg) else 'matches neither'}"
+                        f" (first eager-vs-eager difference at step {k if not np.array_equal(pr, hist[k]) else None})")
 
 
 def test_train_graphs_match_eager(cuda):
