@@ -409,6 +409,24 @@ __device__ __forceinline__ void split_chunk(const uint8_t* buf, const bf16x8 (&x
     }
 }
 
+// hi + lo of a hi/lo accumulator pair.  DF_WIDE_SADD: four v_add_f32 (asm) instead of the
+// two v_pk_add_f32 plain -O3 makes of an f32x4 add (a packed f32 op issues at a quarter of
+// the rate of v_add_f32 beside MFMAs, tools/probe/mfma_valu.hip); the same roundings.  On
+// for the forward unit only (Makefile): config-4 forward 15.83 -> 15.73 M cycles, the
+// logpdf / training-inverse unit lost 0.6% of the config-5 step (gpurun_out/r06n)
+#ifndef DF_WIDE_SADD
+#define DF_WIDE_SADD 0
+#endif
+__device__ __forceinline__ f32x4 add_hilo(const f32x4& a, const f32x4& b) {
+    if constexpr (DF_WIDE_SADD) {
+        f32x4 r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) asm("v_add_f32 %0, %1, %2" : "=v"(r[q]) : "v"(a[q]), "v"(b[q]));
+        return r;
+    }
+    return a + b;
+}
+
 // Planes of accumulator tiles 2c, 2c+1 (inputs 32c + 16(e>>2) + 4g + (e&3)).
 // DF_WIDE_MREM: the remainders on the matrix pipe (uni::split8_mrem, bitwise split8).  Off:
 // this kernel is matrix-pipe bound at one wave per SIMD, and the extra 16x16x16 MFMAs cost
@@ -530,7 +548,7 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
     for (int t = 0; t < TT; ++t)
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
-            const f32x4 v = (DF_WIDE_DIAG & 1) ? acc[t][m & 1] : acc[t][m] + lo[t][m];
+            const f32x4 v = (DF_WIDE_DIAG & 1) ? acc[t][m & 1] : add_hilo(acc[t][m], lo[t][m]);
 #pragma unroll
             for (int r = 0; r < 4; ++r) h[t][m][r] = (DF_WIDE_DIAG & 1) ? v[r] : uni::relu_fast(v[r]);
         }
@@ -559,8 +577,8 @@ __device__ __forceinline__ void eval_net_split(const ChainArgs& a, const WNet& N
     }
 #pragma unroll
     for (int t = 0; t < TT; ++t) {
-        out[t][0] = acc[t][0] + lo[t][0];
-        out[t][1] = acc[t][1] + lo[t][1];
+        out[t][0] = add_hilo(acc[t][0], lo[t][0]);
+        out[t][1] = add_hilo(acc[t][1], lo[t][1]);
     }
 }
 
