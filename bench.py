@@ -46,8 +46,8 @@ PEAK_HBM_GBS = 8000.0
 # HBM bytes per launch of the headline kernel from rocprofv3 PMC counters
 # (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, WRITE_SIZE as is; KiB),
 # measured on the headline workload and committed under profiles/.
-TRAFFIC_PROFILES = {"cfg2": os.path.join("profiles", "r05final_pmc_cfg2.txt"),
-                    "cfg4": os.path.join("profiles", "r05final_pmc_cfg4.txt")}
+TRAFFIC_PROFILES = {"cfg2": os.path.join("profiles", "r06final_pmc_cfg2.txt"),
+                    "cfg4": os.path.join("profiles", "r06final_pmc_cfg4.txt")}
 
 
 def source_sha16():
