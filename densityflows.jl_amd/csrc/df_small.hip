@@ -135,7 +135,8 @@ __device__ __forceinline__ float eval_net(const NetW& w, float xin) {
 // (the two nets of a layer read the same features, RNVP.jl:174-177, and are
 // independent).  Wave 1 hands its outputs over in LDS; wave 0 applies the coupling and
 // keeps the ldj; a barrier after each layer gives wave 1 the updated row.  Both waves
-// write the initial row (identical values), so the first layer needs no barrier.
+// write the initial row (identical values), so a first coupling layer needs no barrier
+// (a first NormalizationLayer does: see the kernel).
 // Each wave issues one net's instructions per layer instead of two.
 // The barriers are bare (lgkmcnt(0) + s_barrier): the LDS row and the handed-over
 // outputs are the only data the waves share; no global load needs to land for them.
@@ -207,6 +208,14 @@ __global__ void __launch_bounds__(64 * NW, 1) small_kernel(ChainArgs a, SmallDes
             v = (diff == 0.f) ? 0.f : (v - blo[q]) / diff;
         }
         if (c < kStride) row[c] = v;
+    }
+    // Both waves write the initial row, so a first coupling layer needs no barrier: wave 0
+    // writes the row only after the handover barrier inside couple().  A first
+    // NormalizationLayer (the inverse pass of a chain that ends with one) is written by
+    // wave 0 without that barrier, and wave 1's initial write could land after it and undo
+    // it, so that layer waits for both waves' initial writes first.
+    if constexpr (NW == 2) {
+        if (dr.i8(SD_OFF(kind) + (FWD ? 0 : NL - 1)) == DF_LAYER_NORM) lds_barrier();
     }
     DF_PH(1);
     float ldjA = 0.f, ldjE = 0.f;  // lane group 0: the sample's chain and element ldj

@@ -605,9 +605,51 @@ def test_step_graph_matches_eager_steps(cuda, path, name):
                 pr = ref.get_params()
                 if not np.array_equal(pr, hist[k]):
                     break
-            pytest.fail(f"step {i} (B = {B}): graph and eager parameters differ; a third eager replay "
+            dif = np.flatnonzero(pg != pe)
+            pytest.fail(f"step {i} (B = {B}): graph and eager parameters differ ({dif.size} of {pe.size}, "
+                        f"indices {dif.min()}..{dif.max()}, max |diff| {np.abs(pg - pe).max():.3g}); a third eager replay "
                         f"{'matches the eager trainer' if np.array_equal(pr, pe) else 'matches the graph trainer' if np.array_equal(pr, pg) else 'matches neither'}"
                         f" (first eager-vs-eager difference at step {k if not np.array_equal(pr, hist[k]) else None})")
+
+
+def test_small_kernel_first_normalization_layer_reproducible(cuda, monkeypatch, capfd):
+    """Regression (round 6): the two-wave small kernel runs the inverse pass of a chain
+    that ends with a NormalizationLayer (the README chain) layer-last-first, so that layer
+    is the first it applies.  Both waves write the initial state row; wave 0 then writes
+    the normalised row, and without a barrier in between wave 1's initial write could land
+    after it and undo it (df_small.hip).  That race made
+    test_step_graph_matches_eager_steps[fused-readme] fail in about half of the runs of this
+    file (gpurun_out/r06y; none in 5 runs with the barrier, r06aa).  Here: the inverse pass
+    (MODE_BWD) and the training gradient (logpdf mode with the per-layer snapshots) at
+    B = 5000 (313 workgroups), repeated, must equal the FAST kernel's, bitwise.  (A timing
+    race: this test alone did not catch it on the unfixed library in three runs, r06ab.)"""
+    import torch
+
+    def run(small):
+        monkeypatch.delenv("DF_SMALL_MAX", raising=False)
+        if not small:
+            monkeypatch.setenv("DF_SMALL_MAX", "0")
+        monkeypatch.setenv("DF_DEBUG_LAUNCH", "1")
+        spec, chain, d, n = _setup("readme", seed=3)
+        B = 5000
+        x, th = _inputs(d, n, B, seed=11)
+        xt = torch.from_numpy(np.ascontiguousarray(x.T)).to(cuda).T
+        tt = torch.from_numpy(np.ascontiguousarray(th.T)).to(cuda).T
+        tr = HIPTrainer(chain.hip(), Adam())
+        outs = []
+        for _ in range(12 if small else 1):
+            z, ldj = dfa.backward(chain, xt, tt)
+            g, _ = _gpu_grad(tr, x, th, cuda)
+            outs.append((z.cpu().numpy().copy(), ldj.cpu().numpy().copy(), g))
+        launches = capfd.readouterr().err
+        assert ("kernel small " in launches) == small, launches
+        monkeypatch.delenv("DF_DEBUG_LAUNCH", raising=False)
+        return outs
+
+    ref = run(False)[0]
+    for k, out in enumerate(run(True)):
+        for what, a, b in zip(("z", "ldj", "gradient"), out, ref):
+            assert np.array_equal(a, b), f"repeat {k}: {what} differs from the FAST kernel's"
 
 
 def test_train_graphs_match_eager(cuda):
