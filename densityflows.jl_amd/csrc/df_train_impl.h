@@ -121,7 +121,15 @@ __device__ __forceinline__ void t_write(float* T, const f32x4 (&v)[HT]) {
     }
 }
 
-__device__ __forceinline__ float hsum4(f32x4 v) { return (v[0] + v[1]) + (v[2] + v[3]); }
+// Scalar f32 adds the compiler cannot pair into v_pk_add_f32: a packed f32 add issues at a
+// quarter of v_add_f32's rate (tools/probe/mfma_pair.hip) and its operand pairs cost moves.
+// Same operations in the same order as the plain expressions.
+__device__ __forceinline__ float fadd(float a, float b) {
+    float r;
+    asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float hsum4(f32x4 v) { return fadd(fadd(v[0], v[1]), fadd(v[2], v[3])); }
 
 __device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -468,7 +476,7 @@ __global__ void __launch_bounds__(train_threads(SPLIT), 1) train_net_kernel(Trai
         for (int t = 0; t < TT; ++t) {
             if constexpr (M4) {  // block b: A = ȳ[lane % 4][s], B = h[lane][s], one sample s per step
                 const f32x4 fa = tread(TA(t), j, g);
-                gbo += hsum4(fa);
+                gbo = fadd(gbo, hsum4(fa));
                 f32x4 yv[4], hv[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -481,7 +489,7 @@ __global__ void __launch_bounds__(train_threads(SPLIT), 1) train_net_kernel(Trai
                     for (int e = 0; e < 4; ++e) gWo4 = mfma4x4(yv[q][e], hv[q][e], gWo4);
             } else {
                 const f32x4 fa = tread(TA(t), j, g);
-                gbo += hsum4(fa);
+                gbo = fadd(gbo, hsum4(fa));
 #pragma unroll
                 for (int mb = 0; mb < HT; ++mb) {
                     const f32x4 fb = tread(TB(t), 16 * mb + j, g);
@@ -537,7 +545,7 @@ __global__ void __launch_bounds__(train_threads(SPLIT), 1) train_net_kernel(Trai
                 for (int m = 0; m < HT; ++m) {
                     fa[m] = tread(TA(t), 16 * m + j, g);
                     fb[m] = tread(TB(t), 16 * m + j, g);
-                    gbh[m] += hsum4(fa[m]);
+                    gbh[m] = fadd(gbh[m], hsum4(fa[m]));
                 }
                 if constexpr (SPLIT && DF_TRAIN_DW1_CONTIG) {
                     // Planes of 4 samples in one 6-dword run per row tile, [p1 p0 p2]: its
@@ -629,7 +637,7 @@ __global__ void __launch_bounds__(train_threads(SPLIT), 1) train_net_kernel(Trai
                     dv[q] = tread(TA(t), lrow, q);
                     xv[q] = tread(TB(t), lane & 3, q);
                 }
-                gb0l += (hsum4(dv[0]) + hsum4(dv[1])) + (hsum4(dv[2]) + hsum4(dv[3]));
+                gb0l = fadd(gb0l, fadd(fadd(hsum4(dv[0]), hsum4(dv[1])), fadd(hsum4(dv[2]), hsum4(dv[3]))));
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -639,7 +647,7 @@ __global__ void __launch_bounds__(train_threads(SPLIT), 1) train_net_kernel(Trai
 #pragma unroll
                 for (int m = 0; m < HT; ++m) {
                     const f32x4 fa = tread(TA(t), 16 * m + j, g);
-                    gb0[m] += hsum4(fa);
+                    gb0[m] = fadd(gb0[m], hsum4(fa));
 #pragma unroll
                     for (int q = 0; q < 4; ++q) gW0[m] = mfma4(fa[q], fb[q], gW0[m]);
                 }
