@@ -20,6 +20,12 @@ using impl::mfma4;
 #ifndef DF_LT_MREM
 #define DF_LT_MREM 0
 #endif
+#ifndef DF_LDENSE_MASK_PF
+#define DF_LDENSE_MASK_PF 1
+#endif
+#ifndef DF_LDENSE_ZV_EARLY
+#define DF_LDENSE_ZV_EARLY 1
+#endif
 #ifndef DF_LDW_MREM  // the split dW kernel's own choice (its matrix pipe idles in the split phase)
 #define DF_LDW_MREM DF_LT_MREM
 #endif
@@ -154,6 +160,16 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
         constexpr int HR = (MT < 8 ? MT : 8) / (T > 2 ? 2 : 1);  // σ' arguments in flight
         const int64_t s0h = valid[0] ? smp[0] : a.batch - 1;
         f32x4 h0[kDact ? HR : 1];
+        // MASK (DF_LDENSE_MASK_PF): tile 0's relu-mask words are loaded during the last chunk
+        // too, into the registers of the B rows that chunk no longer prefetches
+        constexpr bool kMaskPf = MASK && DF_LDENSE_MASK_PF;
+        auto mask_words = [&](int64_t s, uint4 (&mq)[4]) {
+            const int sl = (int)(s & 31);
+            const uint32_t* mb = a.hmask + (s >> 5) * 256 + 16 * ((sl >> 2) & 3) + 4 * g;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) mq[w] = *reinterpret_cast<const uint4*>(mb + 64 * w);
+        };
+        uint4 mq0[kMaskPf ? 4 : 1];
         if constexpr (SPLIT && IN == LIN_BUF) {
             f32x4 xn1[T];
             load_x(1, xn1);
@@ -178,6 +194,9 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
                         for (int m = 0; m < HR; ++m)
                             h0[m] = *reinterpret_cast<const f32x4*>(a.hprev + s0h * a.ld_h + 4 * g + 16 * m);
                     }
+                }
+                if constexpr (kMaskPf) {
+                    if (c + 1 == nchunks) mask_words(s0h, mq0);
                 }
                 const uint8_t* wb = buf + lane * 16;
 #pragma unroll
@@ -254,15 +273,38 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
                 // the σ' arguments of the whole tile are loaded at once (a padding
                 // sample reads the last row; its δ is zeroed and never stored)
                 const int64_t s = valid[t] ? smp[t] : a.batch - 1;
+                // XB: the z̄ entries x̄ adds to, read before the δ epilogue (DF_LDENSE_ZV_EARLY: their
+                // latency then overlaps it and the x̄ product; z̄ and the δ rows are separate buffers)
+                uint32_t zoff[4];  // the columns of features 16m + 4g + q, a byte per q
+                float zv[4][4];
+                auto load_zv = [&]() {
+                    const uint8_t* zcol = w0t_lds + ((SPLIT && a.w0s) ? (a.w0t_nkq / 2) * a.w0t_mt * 3072
+                                                                       : a.w0t_mt * a.w0t_nkq * 1024);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        if (m < a.w0t_mt) {
+                            zoff[m] = *reinterpret_cast<const uint32_t*>(zcol + 16 * m + 4 * g);
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const uint32_t c = (zoff[m] >> (8 * q)) & 0xffu;
+                                zv[m][q] = a.zbar[s * a.d + (c != 0xffu ? c : 0u)];
+                            }
+                        }
+                    }
+                };
+                if constexpr (XB && DF_LDENSE_ZV_EARLY) load_zv();
                 if constexpr (MASK) {  // relu σ' from the mask of the H0-recomputing split dW1 (no H read)
                     // sample s = 32S + 16tt + 4g' + r: rows 16(4w + mm) + 4g + q in dwords
                     // (S·4 + w)·64 + 16g' + 4g + q, bit 4(2mm + tt) + r (df_ltrain.h LdwArgs::hmask)
                     const int sl = (int)(s & 31);
                     const int sh = 4 * ((sl >> 4) & 1) + (sl & 3);
-                    const uint32_t* mb = a.hmask + (s >> 5) * 256 + 16 * ((sl >> 2) & 3) + 4 * g;
                     uint4 mq[4];
+                    if (kMaskPf && t == 0) {
 #pragma unroll
-                    for (int w = 0; w < 4; ++w) mq[w] = *reinterpret_cast<const uint4*>(mb + 64 * w);
+                        for (int w = 0; w < 4; ++w) mq[w] = mq0[kMaskPf ? w : 0];
+                    } else {
+                        mask_words(s, mq);
+                    }
 #pragma unroll
                     for (int m = 0; m < MT; ++m) {
                         f32x4 v = acc[t][m];
@@ -302,21 +344,7 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
                     // The z̄ entries it adds to are read ahead of the product (their latency
                     // overlaps its MFMAs), all loads ahead of all stores: distinct features
                     // of a sample map to distinct state slots (axis_nn).
-                    const uint8_t* zcol = w0t_lds + ((SPLIT && a.w0s) ? (a.w0t_nkq / 2) * a.w0t_mt * 3072
-                                                                       : a.w0t_mt * a.w0t_nkq * 1024);
-                    uint32_t zoff[4];  // the columns of features 16m + 4g + q, a byte per q
-                    float zv[4][4];
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        if (m < a.w0t_mt) {
-                            zoff[m] = *reinterpret_cast<const uint32_t*>(zcol + 16 * m + 4 * g);
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                const uint32_t c = (zoff[m] >> (8 * q)) & 0xffu;
-                                zv[m][q] = a.zbar[s * a.d + (c != 0xffu ? c : 0u)];
-                            }
-                        }
-                    }
+                    if constexpr (!DF_LDENSE_ZV_EARLY) load_zv();
                     f32x4 xb[4];
 #pragma unroll
                     for (int m = 0; m < 4; ++m) xb[m] = f32x4{0.f, 0.f, 0.f, 0.f};
