@@ -479,8 +479,14 @@ __global__ void __launch_bounds__(NW * 64, 1) ldense_kernel(LDenseArgs a) {
 // f32 MFMAs per block; the 8 waves are summed in LDS in wave order and each workgroup
 // writes its partial row (bitwise reproducible, like every other dW).
 constexpr int kFrontDwoTS = 16 * kTS;  // floats of one 16-row transpose block
+// H blocks moved through LDS per round trip (DF_FRONT_DWO_NB): NB writes, one wait, NB reads
+// instead of a wait before and after every block (two lgkmcnt(0) per 16 rows of H)
+#ifndef DF_FRONT_DWO_NB
+#define DF_FRONT_DWO_NB 4
+#endif
+constexpr int kDwoNB = DF_FRONT_DWO_NB;
 size_t front_dwo_lds_bytes(int ht) {
-    const size_t tr = (size_t)kWavesPerBlock * 2 * kFrontDwoTS * 4;        // ȳ and H blocks per wave
+    const size_t tr = (size_t)kWavesPerBlock * (1 + kDwoNB) * kFrontDwoTS * 4;  // ȳ and H blocks per wave
     const size_t red = (size_t)16 * (16 * ht + 4) * 4 + (size_t)kWavesPerBlock * 256 * 4;  // dW rows + db lanes
     return tr > red ? tr : red;
 }
@@ -497,8 +503,8 @@ __device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, 
 #endif
     constexpr bool HPF = !DWO || DF_FRONT_DWO_PF;  // H of the next tile prefetched
     float* dscr = reinterpret_cast<float*>(smem + 2 * HT * MTO * 1024);  // DWO scratch (front_dwo_lds_bytes)
-    float* Ty = dscr + wave * 2 * kFrontDwoTS;  // this wave's ȳ block [o][sample] ...
-    float* Th = Ty + kFrontDwoTS;               // ... and H block [row][sample]
+    float* Ty = dscr + wave * (1 + kDwoNB) * kFrontDwoTS;  // this wave's ȳ block [o][sample] ...
+    float* Th = Ty + kFrontDwoTS;                          // ... and kDwoNB H blocks [row][sample]
     f32x4 gwo[DWO ? HT : 1];                    // dW[o = 4g + r][16kq + j]
     float gbo[4] = {0.f, 0.f, 0.f, 0.f};        // Σ ȳ[4g + r] over this lane's samples
 #pragma unroll
@@ -667,15 +673,25 @@ __device__ __forceinline__ void couple_body(const LDenseArgs& a, uint8_t* smem, 
             for (int q = 0; q < 4; ++q) gbo[q] += dy[0][q];
             const f32x4 ya = trn::tread(Ty, j, g);  // ȳ[o = j][samples 4g .. 4g + 3]
 #pragma unroll
-            for (int kq = 0; kq < HT; ++kq) {
-                if (kq < a.nkq) {
-                    const f32x4 hk[1] = {h[kq]};
-                    trn::lds_order();
-                    trn::t_write<1>(Th, hk);
-                    trn::lds_order();
-                    const f32x4 hb = trn::tread(Th, j, g);  // H[16kq + j][samples 4g ..]
+            for (int k0 = 0; k0 < HT; k0 += kDwoNB) {
+                trn::lds_order();  // the previous group's reads returned before its blocks are rewritten
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) gwo[kq] = mfma4(ya[q], hb[q], gwo[kq]);
+                for (int b = 0; b < kDwoNB; ++b) {
+                    const int kq = k0 + b;
+                    if (kq < HT && kq < a.nkq) {
+                        const f32x4 hk[1] = {h[kq < HT ? kq : 0]};
+                        trn::t_write<1>(Th + b * kFrontDwoTS, hk);
+                    }
+                }
+                trn::lds_order();
+#pragma unroll
+                for (int b = 0; b < kDwoNB; ++b) {
+                    const int kq = k0 + b;
+                    if (kq < HT && kq < a.nkq) {
+                        const f32x4 hb = trn::tread(Th + b * kFrontDwoTS, j, g);  // H[16kq + j][samples 4g ..]
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) gwo[kq < HT ? kq : 0] = mfma4(ya[q], hb[q], gwo[kq < HT ? kq : 0]);
+                    }
                 }
             }
         }
