@@ -9,6 +9,7 @@ and per tile t of the epilogue +11 + 4t tile start, +12 + 4t δ0 stored, +13 + 4
 issued, +14 + 4t z̄ stored; 120 after the final drain.  The last launch of a config-5
 gradient (net 0's W1ᵀδ1) is the one read back.
 usage: python tools/ldense_stamps.py [batch]
+       python tools/ldense_stamps.py --ldw [batch]   (the split dW1 kernel, tools/ldw_stamps_patch.py)
 """
 import ctypes
 import os
@@ -20,13 +21,31 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def ldw_report(st):
+    """tools/ldw_stamps_patch.py stamps: per wave, cycles of each step's phases."""
+    for wg in range(2):
+        t0 = st[wg, :, 0].min()
+        print(f"workgroup {128 * wg}: per step (wait+barrier / split / barrier / MFMA issue), cycles")
+        for w in range(4):
+            row = st[wg, w]
+            parts = []
+            for k in range(31):
+                ev = row[1 + 4 * k:5 + 4 * k + 1] - t0
+                if row[1 + 4 * k] == 0 or row[5 + 4 * k] == 0:
+                    break
+                prev = row[4 * k] - t0 if k else 0
+                parts.append(f"{ev[0] - prev}/{ev[1] - ev[0]}/{ev[2] - ev[1]}/{ev[3] - ev[2]}")
+            print(f"  w{w} end {row[127] - t0}: " + " ".join(parts))
+
+
 def main():
     import torch
 
     import bench
     from densityflows_amd.train import Adam, HIPTrainer
 
-    B = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
+    args = [a for a in sys.argv[1:] if a != "--ldw"]
+    B = int(args[0]) if args else 1 << 18
     dev = torch.device("cuda", 0)
     d, n, _ = bench.CONFIGS["cfg4"]
     chain = bench.build_chain("cfg4")
@@ -41,6 +60,12 @@ def main():
     for rep in range(3):
         tr.gradient(x, th, B, B)
         torch.cuda.synchronize()
+        if LDW:
+            wb = np.zeros(2 * 4 * 128, np.uint64)
+            assert lib.df_diag_ldw_stamps(wb.ctypes.data_as(ctypes.c_void_p)) == 0
+            print(f"rep {rep}")
+            ldw_report(wb.reshape(2, 4, 128).astype(np.int64))
+            continue
         rc = lib.df_diag_ldense_stamps(buf.ctypes.data_as(ctypes.c_void_p))
         assert rc == 0, rc
         st = buf.reshape(2, 8, 128).astype(np.int64)
@@ -63,6 +88,8 @@ def main():
                                    for t in range(2)) + "]")
                 print("  " + "\n    ".join(out))
 
+
+LDW = "--ldw" in sys.argv
 
 if __name__ == "__main__":
     main()
